@@ -1,0 +1,201 @@
+/*
+ * picard_mi355x.h — C ABI of the MI355X-native Picard / Picard-O ICA solver.
+ *
+ * This is the drop-in boundary for the hot path of lmmx/picard-ica v0.1.6.
+ * The reference is a Rust crate; its public API and the operator calls inside
+ * core::run are what these entry points replace (file:line in the reference):
+ *
+ *   pc_fit / pc_fit_default   ← Picard::fit_with_config / Picard::fit   (src/solver.rs:45 / :33)
+ *   pc_transform              ← Picard::transform                      (src/solver.rs:199)
+ *   pc_full_unmixing          ← PicardResult::full_unmixing            (src/result.rs:39)
+ *   pc_mixing                 ← PicardResult::mixing                   (src/result.rs:49)
+ *   pc_amari_distance         ← utils::amari_distance                  (src/utils.rs:82)
+ *   pc_permute                ← utils::permute                         (src/utils.rs:16)
+ *   pc_config_default         ← impl Default for PicardConfig          (src/config.rs:64-85)
+ *   pc_config_validate        ← PicardConfig::validate                 (src/config.rs:104-142)
+ *   pc_result_free            ← Drop for PicardResult                  (src/result.rs:7)
+ *   pc_error_message          ← impl Display for PicardError           (src/error.rs:44-74)
+ *
+ * The operator boundary inside core::run (src/core.rs:162-174), i.e. what
+ * the HIP kernels replace (score_and_der core.rs:215, the .dot GEMMs
+ * core.rs:124/218/274, compute_loss core.rs:39-85, center/whiten
+ * whitening.rs:24-116):
+ *
+ *   pc_ctx_eval               one fused pass over X: Y = W·(X−μ) → ψ, ψ′, ℓ →
+ *                             G_raw = ψ·Yᵀ [, H_raw = ψ′·(Y∘Y)ᵀ], Σψ′, Σℓ, Σy²
+ *   pc_ctx_rowsum / pc_ctx_gram   centering and the whitening Gram X·Xᵀ
+ *   pc_ctx_sources            Y = W·(X−μ) materialised (PicardResult.sources)
+ *
+ * Conventions: every matrix is row-major, contiguous, float64. Rows are
+ * features/components, columns are samples (src/solver.rs:29,40). Inputs
+ * are borrowed read-only; result buffers are owned by the library and
+ * released by pc_result_free. Calls are synchronous. A context is driven by
+ * one host thread. Errors are returned as pc_status codes with the message
+ * text of src/error.rs:44-74 written into (err, errlen) when err != NULL.
+ */
+#ifndef PICARD_MI355X_H
+#define PICARD_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
+typedef enum {
+  PC_OK = 0,
+  PC_ERR_INVALID_DIMENSIONS = 1,
+  PC_ERR_SINGULAR_MATRIX = 2,
+  PC_ERR_COMPUTATION = 3,
+  PC_ERR_INVALID_CONFIG = 4,
+  PC_ERR_NOT_CONVERGED = 5
+} pc_status;
+
+/* src/density.rs:137-144 DensityType */
+typedef enum { PC_DENSITY_TANH = 0, PC_DENSITY_EXP = 1, PC_DENSITY_CUBE = 2 } pc_density_kind;
+
+typedef struct {
+  int32_t kind;   /* pc_density_kind */
+  double alpha;   /* Tanh/Exp alpha (density.rs:34,75); ignored for Cube */
+} pc_density;
+
+/* src/config.rs:11-62 — the 16 fields; Option<T> → has_* flag + value */
+typedef struct {
+  pc_density density;
+  int32_t has_n_components; uint64_t n_components;
+  int32_t ortho;
+  int32_t has_extended; int32_t extended;
+  int32_t whiten;
+  int32_t centering;
+  uint64_t max_iter;
+  double tol;
+  uint64_t m;
+  uint64_t ls_tries;
+  double lambda_min;
+  const double* w_init; uint64_t w_init_rows; uint64_t w_init_cols; /* NULL = None */
+  int32_t has_fastica_it; uint64_t fastica_it;
+  int32_t has_jade_it; uint64_t jade_it;
+  int32_t has_random_state; uint64_t random_state;
+  int32_t verbose;
+  /* MI355X additions (not in the reference): */
+  int32_t device;          /* HIP device ordinal for pc_fit (default 0) */
+  int32_t want_sources;    /* materialise PicardResult.sources (default 1) */
+} pc_config;
+
+/* src/result.rs:7-33 — buffers are library-owned, NULL for None */
+typedef struct {
+  double* whitening; uint64_t whitening_rows, whitening_cols; /* K: n_components × n_features */
+  double* unmixing;  uint64_t unmixing_rows,  unmixing_cols;  /* W: n_components × n_components */
+  double* sources;   uint64_t sources_rows,   sources_cols;   /* Y: n_components × n_samples */
+  double* mean;      uint64_t mean_len;                       /* μ: n_features */
+  uint64_t n_iterations;
+  int32_t converged;
+  double gradient_norm;
+  double* signs;     uint64_t signs_len;                      /* extended only */
+  /* MI355X additions: work counters for the iterations-to-tol metric */
+  uint64_t n_evaluations;  /* fused passes over X issued by core::run */
+} pc_result;
+
+/* ---- public API (mirrors src/lib.rs:50-57) --------------------------- */
+void pc_config_default(pc_config* cfg);
+int pc_config_validate(const pc_config* cfg, char* err, size_t errlen);
+
+int pc_fit(const double* x, uint64_t n_features, uint64_t n_samples, const pc_config* cfg,
+           pc_result* out, char* err, size_t errlen);
+int pc_fit_default(const double* x, uint64_t n_features, uint64_t n_samples, pc_result* out,
+                   char* err, size_t errlen);
+int pc_transform(const double* x, uint64_t n_features, uint64_t n_samples, const pc_result* res,
+                 double* out /* n_components × n_samples */, int32_t device, char* err, size_t errlen);
+int pc_full_unmixing(const pc_result* res, double* out /* n_components × n_features */);
+int pc_mixing(const pc_result* res, double* out /* n_features × n_components */);
+void pc_result_free(pc_result* res);
+double pc_amari_distance(const double* w, const double* a, uint64_t n);
+void pc_permute(const double* a, uint64_t n, int32_t scale, double* out);
+const char* pc_error_name(int status);
+const char* pc_version(void);
+
+/* ---- device context: X resident in HBM, optionally T-sharded over ranks --- */
+typedef struct pc_ctx pc_ctx;
+
+/* RCCL bootstrap for one-process-per-GPU runs: rank 0 calls pc_rccl_unique_id,
+ * the 128-byte id is broadcast by the caller (e.g. torch.distributed), every
+ * rank then creates its context with it. world_size == 1 needs no id. */
+int pc_rccl_unique_id(char id_out[128]);
+
+/* Each rank owns the samples [t0, t0 + n_local) of a global matrix with
+ * n_total samples (contiguous T blocks). */
+int pc_ctx_create(int32_t device, int32_t rank, int32_t world_size, const char* rccl_id /* or NULL */,
+                  pc_ctx** out, char* err, size_t errlen);
+void pc_ctx_destroy(pc_ctx* ctx);
+/* copy a host shard (n_features × n_local, row-major) into HBM */
+int pc_ctx_load(pc_ctx* ctx, const double* x_shard, uint64_t n_features, uint64_t n_local,
+                uint64_t n_total, uint64_t t0, char* err, size_t errlen);
+/* generate the benches/benchmarks.rs:8-35 mixture directly in HBM: this rank's
+ * contiguous shard of the global (n_features × n_total) X for `seed`; the
+ * mixing matrix A (n_features²) is written to a_out when not NULL */
+int pc_ctx_generate(pc_ctx* ctx, uint64_t n_features, uint64_t n_total, uint64_t seed,
+                    double* a_out, char* err, size_t errlen);
+/* copy this rank's shard back to the host (n_features × n_local) */
+int pc_ctx_download(pc_ctx* ctx, double* x_shard_out);
+uint64_t pc_ctx_n_local(const pc_ctx* ctx);
+uint64_t pc_ctx_t0(const pc_ctx* ctx);
+
+/* Operator boundary. All statistics are summed over every rank's shard
+ * (one RCCL all-reduce per call when world_size > 1). */
+enum { PC_EVAL_NEED_H = 1u };
+/* stats = [G_raw (nc×nc) | H_raw (nc×nc, only with PC_EVAL_NEED_H) | Σψ′ (nc) | Σℓ (nc) | Σy² (nc)] */
+int pc_ctx_eval(pc_ctx* ctx, const double* w /* nc × n_features */, uint64_t nc,
+                const double* mu /* n_features or NULL */, pc_density density, uint32_t flags,
+                double* stats, char* err, size_t errlen);
+int pc_ctx_rowsum(pc_ctx* ctx, double* out /* n_features */, char* err, size_t errlen);
+int pc_ctx_gram(pc_ctx* ctx, const double* mu /* or NULL */, double* out /* nf × nf */,
+                char* err, size_t errlen);
+/* this rank's shard of Y = W·(X−μ) → host (nc × n_local) */
+int pc_ctx_sources(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, double* out,
+                   char* err, size_t errlen);
+/* Σ_t z_p z_q over the pair products z_(i,j) = y_i y_j (i ≤ j) of Y = W·(X−μ):
+ * the fourth-moment matrix JADE's cumulants are built from (src/jade.rs:91-113).
+ * out: P × P with P = nc(nc+1)/2, pairs in row-major (i ≤ j) order. */
+int pc_ctx_moments4(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, double* out,
+                    char* err, size_t errlen);
+
+/* Stepping solver over a context: pc_fit's pipeline (solver.rs:45-189) split
+ * so that a caller can time individual Picard iterations (core.rs:211-391).
+ * pc_solver_step runs ONE iteration; *done becomes 1 on convergence or when
+ * max_iter iterations have run. pc_solver_finish fills the result (sources
+ * only when cfg->want_sources, and then only this rank's shard). */
+typedef struct pc_solver pc_solver;
+int pc_solver_create(pc_ctx* ctx, const pc_config* cfg, pc_solver** out, char* err, size_t errlen);
+int pc_solver_step(pc_solver* s, int32_t* done, char* err, size_t errlen);
+int pc_solver_finish(pc_solver* s, pc_result* out, char* err, size_t errlen);
+void pc_solver_destroy(pc_solver* s);
+/* last iteration's: loss, gradient norm, passes issued in that iteration */
+void pc_solver_last(const pc_solver* s, double* loss, double* gradient_norm, uint64_t* n_evals);
+
+/* Host-driver hook: run the same solver pipeline over caller-supplied
+ * evaluation callbacks instead of the HIP context. Used by the CPU test suite
+ * to check the host logic (core::run, L-BFGS, line search, whitening) without
+ * a GPU; the product path never uses it. */
+typedef struct {
+  void* user;
+  uint64_t n_features, n_samples;
+  int (*rowsum)(void* user, double* out);
+  int (*gram)(void* user, const double* mu, double* out);
+  int (*eval)(void* user, const double* w, uint64_t nc, const double* mu, pc_density density,
+              uint32_t flags, double* stats);
+  int (*sources)(void* user, const double* w, uint64_t nc, const double* mu, double* out);
+  int (*moments4)(void* user, const double* w, uint64_t nc, const double* mu, double* out);
+} pc_host_evaluator;
+int pc_fit_with_evaluator(const pc_host_evaluator* ev, const pc_config* cfg, pc_result* out,
+                          char* err, size_t errlen);
+
+/* Timing of the most recent pc_ctx_eval on the context's stream, measured
+ * with HIP events around the fused-pass kernel and the whole call. */
+void pc_ctx_last_timing(const pc_ctx* ctx, double* kernel_ms, double* call_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PICARD_MI355X_H */

@@ -1,0 +1,880 @@
+// MI355X (gfx950) device side of the Picard solver.
+//
+// The hot path is k_eval_fused: ONE pass over the resident X shard computes,
+// for a candidate unmixing map W (nc × nf) and mean μ,
+//     Y = W·(X − μ)                      (core.rs:124 / solver.rs:140, fp64 MFMA)
+//     ψ, ψ′, ℓ = density(Y)              (density.rs:50-130, fp64 VALU, registers only)
+//     G_raw += ψ·Yᵀ                      (core.rs:218, fp64 MFMA)
+//     H_raw += ψ′·(Y∘Y)ᵀ   (non-ortho)   (core.rs:274, fp64 MFMA)
+//     Σψ′, Σℓ, Σy² per row               (core.rs:226,264, :76,:79)
+// Y never touches HBM: each 16×16 Yᵀ tile produced by v_mfma_f64_16x16x4_f64
+// already sits in registers in the A/B operand layout of the next MFMA
+// (lane l, reg r ↔ row l&15, sample 4r + (l>>4)), so ψ and Y are handed to
+// the G-stage waves through LDS without any transpose. Per-workgroup partial
+// sums are reduced by k_reduce in a fixed order (bit-reproducible; no atomics).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "evaluator.hpp"
+
+namespace pcamd {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+enum { DENS_TANH = 0, DENS_EXP = 1, DENS_CUBE = 2, DENS_LINEAR = 3, DENS_NONE = 4 };
+
+#define HIP_OK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      throw computation_error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #expr); \
+  } while (0)
+
+#define RCCL_OK(expr)                                                                        \
+  do {                                                                                       \
+    ncclResult_t r_ = (expr);                                                                \
+    if (r_ != ncclSuccess)                                                                   \
+      throw computation_error(std::string("RCCL: ") + ncclGetErrorString(r_) + " at " #expr); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// density.rs:50-130 per element. psi = ψ(y), dpsi = ψ′(y), ll = ℓ(y).
+// Tanh: one expm1 feeds both tanh(αy) = −em/(2+em)·sign and
+// ℓ = |y| + ln(1 + e^{−2α|y|})/α = |y| + ln(2 + em)/α.
+// ---------------------------------------------------------------------------
+template <int DENS>
+__device__ __forceinline__ void density_eval(double y, double alpha, double& psi, double& dpsi, double& ll) {
+  if constexpr (DENS == DENS_TANH) {
+    // em = e^{-2|αy|} − 1; for α > 0 this is also e^{-2α|y|} − 1 (ℓ's term);
+    // for α < 0, e^{-2α|y|} = 1/(1 + em).
+    const double ay = fabs(y);
+    const double a = alpha * y;
+    const double em = expm1(-2.0 * fabs(a));
+    const double th = copysign(-em / (2.0 + em), a);
+    psi = th;
+    dpsi = alpha * (1.0 - th * th);
+    ll = ay + log(alpha > 0.0 ? 2.0 + em : (2.0 + em) / (1.0 + em)) / alpha;
+  } else if constexpr (DENS == DENS_EXP) {
+    const double y2 = y * y;
+    const double k = exp(-alpha / 2.0 * y2);
+    psi = y * k;
+    dpsi = (1.0 - alpha * y2) * k;
+    ll = -k / alpha;
+  } else if constexpr (DENS == DENS_CUBE) {
+    const double y2 = y * y;
+    psi = y2 * y;
+    dpsi = 3.0 * y2;
+    ll = y2 * y2 / 4.0;
+  } else {  // LINEAR: ψ = y turns G_raw into the Gram Σ y yᵀ
+    psi = y;
+    dpsi = 1.0;
+    ll = 0.0;
+  }
+}
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// The fused pass. NB = 16-row blocks of Y (nc ≤ 16·NB), 8 waves.
+// Block = TB = 16·(8/NB) samples; each wave owns one 16×16 Yᵀ tile of it.
+// ---------------------------------------------------------------------------
+constexpr int FUSED_THREADS = 512;
+constexpr int KSMAX = 32;  // nf ≤ 128 (W fragments live in VGPRs)
+
+template <int NB>
+struct FusedShape {
+  static constexpr int TS = 8 / NB;        // 16-sample sub-blocks per block
+  static constexpr int TB = 16 * TS;       // samples per block
+  static constexpr int NCP = 16 * NB;      // padded rows
+  static constexpr int KK = 4 * TS;        // G-stage k-steps per block
+  static constexpr int GI = NB == 8 ? 4 : 1;
+  static constexpr int GJ = NB >= 4 ? 2 : 1;
+  static constexpr int KSPL = NB == 2 ? 2 : (NB == 1 ? 8 : 1);
+  static constexpr int KKW = KK / KSPL;
+  static constexpr int FRAGS = KK * NB * 64;  // doubles per ψ / y LDS image
+};
+
+__host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
+  return (size_t)(need_h ? 2 : 1) * ncp * ncp + 3 * (size_t)ncp;
+}
+
+template <int NB, bool NEED_H, int DENS>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int nfp,
+             const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
+             uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials) {
+  using S = FusedShape<NB>;
+  constexpr int TS = S::TS, TB = S::TB, NCP = S::NCP, KKW = S::KKW, GI = S::GI, GJ = S::GJ;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int yi = wave % NB, yts = wave / NB;
+
+  extern __shared__ double smem[];
+  double* xs = smem;                         // [TS][nfp][16]
+  double* psis = xs + TS * nfp * 16;         // [KK][NB][64]
+  double* ys = psis + S::FRAGS;              // [KK][NB][64]
+  double* dps = ys + S::FRAGS;               // [KK][NB][64] (NEED_H)
+
+  const int ks_n = nfp >> 2;
+  double wf[KSMAX];
+#pragma unroll
+  for (int ks = 0; ks < KSMAX; ++ks) wf[ks] = ks < ks_n ? Wp[(yi * 16 + lr) * nfp + 4 * ks + lk] : 0.0;
+
+  int gi0, gj0, kk0;
+  if constexpr (NB == 8) { gi0 = (wave >> 2) * 4; gj0 = (wave & 3) * 2; kk0 = 0; }
+  else if constexpr (NB == 4) { gi0 = wave >> 1; gj0 = (wave & 1) * 2; kk0 = 0; }
+  else if constexpr (NB == 2) { gi0 = (wave & 3) >> 1; gj0 = wave & 1; kk0 = (wave >> 2) * KKW; }
+  else { gi0 = 0; gj0 = 0; kk0 = wave * KKW; }
+
+  d4 accg[GI][GJ];
+  d4 acch[GI][GJ];
+#pragma unroll
+  for (int i = 0; i < GI; ++i)
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
+  double rs_dpsi = 0.0, rs_ll = 0.0, rs_y2 = 0.0;
+
+  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const int n2 = nfp * TB / 2;  // double2 elements per X tile
+  constexpr int PRE = 2;        // ≥ n2 / 512 (TS·nfp ≤ 128 is checked on the host)
+
+  double2 pre[PRE];
+  auto load_x = [&](uint64_t b) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      const int e = tid + p * FUSED_THREADS;
+      if (e < n2) {
+        const int k = e / (TB / 2), t = 2 * (e % (TB / 2));
+        if (k < nf && b * TB + t < ldx) pre[p] = *reinterpret_cast<const double2*>(X + (size_t)k * ldx + b * TB + t);
+        else pre[p] = double2{0.0, 0.0};
+      }
+    }
+  };
+  auto store_x = [&](uint64_t b) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      const int e = tid + p * FUSED_THREADS;
+      if (e < n2) {
+        const int k = e / (TB / 2), t = 2 * (e % (TB / 2));
+        const uint64_t tg = b * TB + t;
+        const double m = (k < nf && mu) ? mu[k] : 0.0;
+        double2 v;
+        v.x = (k < nf && tg < n_local) ? pre[p].x - m : 0.0;
+        v.y = (k < nf && tg + 1 < n_local) ? pre[p].y - m : 0.0;
+        *reinterpret_cast<double2*>(xs + ((t >> 4) * nfp + k) * 16 + (t & 15)) = v;
+      }
+    }
+  };
+
+  if (b_begin < b_end) load_x(b_begin);
+  for (uint64_t b = b_begin; b < b_end; ++b) {
+    store_x(b);
+    __syncthreads();  // (A) X tile visible; previous G stage finished everywhere
+    if (b + 1 < b_end) load_x(b + 1);
+
+    // ---- Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over nf
+    d4 yv = d4{0, 0, 0, 0};
+    const double* xrow = xs + (yts * nfp + lk) * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KSMAX; ++ks)
+      if (ks < ks_n) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
+
+    // ---- elementwise density, row sums, hand-off through LDS
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double y = yv[r];
+      double psi, dpsi, ll;
+      density_eval<DENS>(y, alpha, psi, dpsi, ll);
+      const uint64_t tg = b * TB + yts * 16 + 4 * r + lk;
+      if (tg < n_local) { rs_dpsi += dpsi; rs_ll += ll; rs_y2 += y * y; }
+      const int kk = yts * 4 + r;
+      psis[(kk * NB + yi) * 64 + lane] = psi;
+      ys[(kk * NB + yi) * 64 + lane] = y;
+      if constexpr (NEED_H) dps[(kk * NB + yi) * 64 + lane] = dpsi;
+    }
+    __syncthreads();  // (B) ψ / y images complete; X tile no longer read
+
+    // ---- G stage: G_raw[i-blocks][j-blocks] += ψ · Yᵀ over this block's samples
+#pragma unroll
+    for (int q = 0; q < KKW; ++q) {
+      const int kk = kk0 + q;
+      double pa[GI], yf[GJ];
+#pragma unroll
+      for (int i = 0; i < GI; ++i) pa[i] = psis[(kk * NB + gi0 + i) * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < GJ; ++j) yf[j] = ys[(kk * NB + gj0 + j) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < GI; ++i)
+#pragma unroll
+        for (int j = 0; j < GJ; ++j) accg[i][j] = mfma(pa[i], yf[j], accg[i][j]);
+      if constexpr (NEED_H) {
+#pragma unroll
+        for (int i = 0; i < GI; ++i) {
+          const double da = dps[(kk * NB + gi0 + i) * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < GJ; ++j) acch[i][j] = mfma(da, yf[j] * yf[j], acch[i][j]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: per-workgroup partials [G | H | Σψ′ | Σℓ | Σy²]
+  double* out = partials + (size_t)blockIdx.x * fused_partial_stride(NCP, NEED_H);
+  __syncthreads();
+  if constexpr (S::KSPL == 1) {
+#pragma unroll
+    for (int i = 0; i < GI; ++i)
+#pragma unroll
+      for (int j = 0; j < GJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (gi0 + i) * 16 + lk + 4 * r, col = (gj0 + j) * 16 + lr;
+          out[row * NCP + col] = accg[i][j][r];
+          if constexpr (NEED_H) out[NCP * NCP + row * NCP + col] = acch[i][j][r];
+        }
+  } else {
+    // waves that split one G block's k range meet in LDS, summed in wave order
+    double* red = psis;  // KSPL × blocks × 256 (+ the same for H)
+    constexpr int NBLK = NB * NB;
+    const int blk = gi0 * NB + gj0;
+    const int sp = kk0 / KKW;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[(sp * NBLK + blk) * 256 + r * 64 + lane] = accg[0][0][r];
+      if constexpr (NEED_H) red[(S::KSPL + sp) * NBLK * 256 + blk * 256 + r * 64 + lane] = acch[0][0][r];
+    }
+    __syncthreads();
+    if (sp == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double g = 0.0, h = 0.0;
+        for (int s2 = 0; s2 < S::KSPL; ++s2) {
+          g += red[(s2 * NBLK + blk) * 256 + r * 64 + lane];
+          if constexpr (NEED_H) h += red[(S::KSPL + s2) * NBLK * 256 + blk * 256 + r * 64 + lane];
+        }
+        const int row = gi0 * 16 + lk + 4 * r, col = gj0 * 16 + lr;
+        out[row * NCP + col] = g;
+        if constexpr (NEED_H) out[NCP * NCP + row * NCP + col] = h;
+      }
+    }
+    __syncthreads();
+  }
+  // row sums: over the 4 lane groups, then over the TS waves of one row block
+  rs_dpsi += __shfl_xor(rs_dpsi, 16); rs_dpsi += __shfl_xor(rs_dpsi, 32);
+  rs_ll += __shfl_xor(rs_ll, 16);     rs_ll += __shfl_xor(rs_ll, 32);
+  rs_y2 += __shfl_xor(rs_y2, 16);     rs_y2 += __shfl_xor(rs_y2, 32);
+  double* rsb = ys;  // [TS][NCP][3]
+  if (lk == 0) {
+    rsb[(yts * NCP + yi * 16 + lr) * 3 + 0] = rs_dpsi;
+    rsb[(yts * NCP + yi * 16 + lr) * 3 + 1] = rs_ll;
+    rsb[(yts * NCP + yi * 16 + lr) * 3 + 2] = rs_y2;
+  }
+  __syncthreads();
+  double* orow = out + (size_t)(NEED_H ? 2 : 1) * NCP * NCP;
+  for (int e = tid; e < NCP * 3; e += FUSED_THREADS) {
+    const int row = e / 3, c = e % 3;
+    double s = 0.0;
+    for (int ts = 0; ts < TS; ++ts) s += rsb[(ts * NCP + row) * 3 + c];
+    orow[c * NCP + row] = s;
+  }
+}
+
+// Fixed-order sum of per-workgroup partials into the compact stats layout
+// [G nc×nc | H nc×nc | Σψ′ nc | Σℓ nc | Σy² nc].
+__global__ void k_reduce(const double* __restrict__ partials, int nwg, size_t pstride, int ncp, int nc,
+                         bool need_h, double* __restrict__ stats) {
+  const size_t nsq = (size_t)nc * nc;
+  const size_t total = (need_h ? 2 : 1) * nsq + 3 * (size_t)nc;
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  size_t src;
+  if (e < nsq) src = (e / nc) * ncp + e % nc;
+  else if (need_h && e < 2 * nsq) { const size_t f = e - nsq; src = (size_t)ncp * ncp + (f / nc) * ncp + f % nc; }
+  else {
+    const size_t f = e - (need_h ? 2 : 1) * nsq;
+    src = (size_t)(need_h ? 2 : 1) * ncp * ncp + (f / nc) * ncp + f % nc;
+  }
+  double s = 0.0;
+  for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + src];
+  stats[e] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Generic path (shapes the fused kernel does not cover: nc > 128, nf > 128,
+// or few rows with many features). Y is materialised per T-chunk.
+// ---------------------------------------------------------------------------
+// Y = W·(X − μ) (+ ψ, ψ′, ℓ) for chunk columns [c0, c0+cn). One thread per sample.
+template <int DENS>
+__global__ void k_ycomp(const double* __restrict__ X, uint64_t ldx, uint64_t n_valid, int nf, int nc,
+                        const double* __restrict__ W, const double* __restrict__ mu, double alpha,
+                        uint64_t c0, uint64_t cn, double* __restrict__ Y, uint64_t ldy,
+                        double* __restrict__ P, double* __restrict__ D, double* __restrict__ L,
+                        uint64_t ldc) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t >= cn) return;
+  const uint64_t tg = c0 + t;
+  const bool valid = tg < n_valid;
+  constexpr int RB = 8;
+  for (int i0 = 0; i0 < nc; i0 += RB) {
+    double acc[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[r] = 0.0;
+    for (int k = 0; k < nf; ++k) {
+      const double xv = valid ? X[(size_t)k * ldx + tg] - (mu ? mu[k] : 0.0) : 0.0;
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        if (i0 + r < nc) acc[r] = fma(W[(size_t)(i0 + r) * nf + k], xv, acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      if (i0 + r >= nc) break;
+      const double y = acc[r];
+      if (Y) Y[(size_t)(i0 + r) * ldy + t] = y;
+      if constexpr (DENS != DENS_NONE) {
+        double psi, dpsi, ll;
+        density_eval<DENS>(y, alpha, psi, dpsi, ll);
+        P[(size_t)(i0 + r) * ldc + t] = psi;
+        D[(size_t)(i0 + r) * ldc + t] = valid ? dpsi : 0.0;
+        L[(size_t)(i0 + r) * ldc + t] = valid ? ll : 0.0;
+      }
+    }
+  }
+}
+
+// out[s][i][j] += Σ_{t in split s} A[i][t]·B[j][t]  (B squared when SQ)
+// 16×16 threads, each a 4×4 output micro-tile of a 64×64 tile; K staged 32 wide.
+template <bool SQ>
+__global__ void __launch_bounds__(256) k_gemm_nt(const double* __restrict__ A, const double* __restrict__ B,
+                                                 uint64_t ld, int m, uint64_t kn, int splits,
+                                                 double* __restrict__ out) {
+  __shared__ double as[64][33];
+  __shared__ double bs[64][33];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int tiles = (m + 63) / 64;
+  const int tile = blockIdx.x % (tiles * tiles), s = blockIdx.x / (tiles * tiles);
+  const int ti = tile / tiles, tj = tile % tiles;
+  const uint64_t per = (kn + splits - 1) / splits;
+  const uint64_t k0 = (uint64_t)s * per, k1 = std::min<uint64_t>(kn, k0 + per);
+  double acc[4][4] = {};
+  for (uint64_t kb = k0; kb < k1; kb += 32) {
+    for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+      const int r = e / 32, c = e % 32;
+      const int gi = ti * 64 + r, gj = tj * 64 + r;
+      const uint64_t kk = kb + c;
+      as[r][c] = (gi < m && kk < k1) ? A[(size_t)gi * ld + kk] : 0.0;
+      double bv = (gj < m && kk < k1) ? B[(size_t)gj * ld + kk] : 0.0;
+      bs[r][c] = SQ ? bv * bv : bv;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int c = 0; c < 32; ++c) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { av[u] = as[ty * 4 + u][c]; bv[u] = bs[tx * 4 + u][c]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] = fma(av[u], bv[v], acc[u][v]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int gi = ti * 64 + ty * 4 + u, gj = tj * 64 + tx * 4 + v;
+      if (gi < m && gj < m) out[((size_t)s * m + gi) * m + gj] += acc[u][v];
+    }
+}
+
+// per-row sums over the chunk: acc[which][row] += Σ_t src_which[row][t]
+__global__ void k_rowsums_chunk(const double* __restrict__ D, const double* __restrict__ L,
+                                const double* __restrict__ Y, uint64_t ldc, uint64_t ldy, uint64_t cn,
+                                uint64_t n_valid_in_chunk, double* __restrict__ acc, int nc) {
+  const int row = blockIdx.x, which = blockIdx.y;
+  __shared__ double red[256];
+  double s = 0.0;
+  for (uint64_t t = threadIdx.x; t < cn; t += blockDim.x) {
+    if (which == 0) s += D[(size_t)row * ldc + t];
+    else if (which == 1) s += L[(size_t)row * ldc + t];
+    else { const double y = t < n_valid_in_chunk ? Y[(size_t)row * ldy + t] : 0.0; s += y * y; }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) acc[which * nc + row] += red[0];
+}
+
+__global__ void k_sum_slabs(const double* __restrict__ slabs, int splits, size_t n, double* __restrict__ out) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double s = 0.0;
+  for (int k = 0; k < splits; ++k) s += slabs[(size_t)k * n + e];
+  out[e] = s;
+}
+
+// Row sums Σ_t X[k][t] over this shard: partials[wg][k], T split over workgroups.
+__global__ void k_rowsum(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, uint64_t per,
+                         double* __restrict__ partials) {
+  __shared__ double red[256];
+  const uint64_t t0 = blockIdx.x * per, t1 = std::min<uint64_t>(n_local, t0 + per);
+  for (int k = 0; k < nf; ++k) {
+    double s = 0.0;
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) s += X[(size_t)k * ldx + t];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[(size_t)blockIdx.x * nf + k] = red[0];
+    __syncthreads();
+  }
+}
+
+// Fourth moments for JADE: out[p][q] += Σ_t z_p z_q, z_(i≤j) = y_i y_j, over a Y chunk.
+__global__ void __launch_bounds__(256) k_moments4(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc,
+                                                  const int* __restrict__ pi, const int* __restrict__ pj, int np,
+                                                  double* __restrict__ out) {
+  __shared__ double za[32][65];
+  __shared__ double zb[32][65];
+  const int tiles = (np + 31) / 32;
+  const int ti = blockIdx.x / tiles, tj = blockIdx.x % tiles;
+  if (tj < ti) return;  // symmetric: upper tiles only
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[2][2] = {};
+  for (uint64_t t0 = 0; t0 < cn; t0 += 64) {
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int r = e / 64, c = e % 64;
+      const uint64_t t = t0 + c;
+      const int p = ti * 32 + r, q = tj * 32 + r;
+      za[r][c] = (p < np && t < cn) ? Y[(size_t)pi[p] * ldy + t] * Y[(size_t)pj[p] * ldy + t] : 0.0;
+      zb[r][c] = (q < np && t < cn) ? Y[(size_t)pi[q] * ldy + t] * Y[(size_t)pj[q] * ldy + t] : 0.0;
+    }
+    __syncthreads();
+    for (int c = 0; c < 64; ++c) {
+      const double a0 = za[ty * 2][c], a1 = za[ty * 2 + 1][c];
+      const double b0 = zb[tx * 2][c], b1 = zb[tx * 2 + 1][c];
+      acc[0][0] = fma(a0, b0, acc[0][0]); acc[0][1] = fma(a0, b1, acc[0][1]);
+      acc[1][0] = fma(a1, b0, acc[1][0]); acc[1][1] = fma(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+  for (int u = 0; u < 2; ++u)
+    for (int v = 0; v < 2; ++v) {
+      const int p = ti * 32 + ty * 2 + u, q = tj * 32 + tx * 2 + v;
+      if (p < np && q < np) out[(size_t)p * np + q] += acc[u][v];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic mixture (benches/benchmarks.rs:8-35), generated in HBM.
+// S[i][t] from LCG state number i·T + t + 1 (jump-ahead per column, then the
+// fixed affine map of T steps per row), Laplace by inverse CDF; u == 0 is
+// replaced by 2^-32 (see oracle/datagen.py).
+// ---------------------------------------------------------------------------
+struct Affine { uint64_t a, c; };
+__host__ __device__ inline Affine lcg_jump(uint64_t n) {
+  uint64_t a = 6364136223846793005ull, c = 1ull, ra = 1ull, rc = 0ull;
+  while (n) {
+    if (n & 1ull) { ra = ra * a; rc = rc * a + c; }
+    c = c * a + c;
+    a = a * a;
+    n >>= 1;
+  }
+  return {ra, rc};
+}
+
+__device__ __forceinline__ double laplace_of(uint64_t st) {
+  double u = (double)(st >> 33) / 2147483648.0;
+  if (u == 0.0) u = 0x1p-32;
+  return u < 0.5 ? log(2.0 * u) : -log(2.0 * (1.0 - u));
+}
+
+__global__ void k_gen_sources(double* __restrict__ S, uint64_t lds, int nf, uint64_t t_begin, uint64_t cn,
+                              uint64_t seed, uint64_t jump_a, uint64_t jump_c) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t >= cn) return;
+  const Affine j = lcg_jump(t_begin + t + 1);
+  uint64_t st = j.a * seed + j.c;
+  for (int i = 0; i < nf; ++i) {
+    S[(size_t)i * lds + t] = laplace_of(st);
+    st = jump_a * st + jump_c;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Device context: one GPU, one X shard, optional RCCL communicator.
+// ---------------------------------------------------------------------------
+struct DeviceCtx : Evaluator {
+  int device = 0, rank = 0, world = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  double* X = nullptr;
+  uint64_t nf = 0, n_local_ = 0, ldx = 0, n_total = 0, t0 = 0;
+  int n_cu = 256;
+  // scratch
+  double* d_w = nullptr; size_t cap_w = 0;
+  double* d_mu = nullptr; size_t cap_mu = 0;
+  double* d_part = nullptr; size_t cap_part = 0;
+  double* d_stats = nullptr; size_t cap_stats = 0;
+  double* d_chunk = nullptr; size_t cap_chunk = 0;
+  hipEvent_t ev[4];
+  double last_kernel_ms = 0, last_call_ms = 0;
+
+  DeviceCtx(int dev, int rk, int ws, const char* uid) : device(dev), rank(rk), world(ws) {
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, device));
+    n_cu = prop.multiProcessorCount;
+    if (world > 1) {
+      if (!uid) throw computation_error("world_size > 1 needs an RCCL unique id");
+      ncclUniqueId id;
+      std::memcpy(&id, uid, sizeof id);
+      RCCL_OK(ncclCommInitRank(&comm, world, id, rank));
+    }
+  }
+  ~DeviceCtx() override {
+    (void)hipSetDevice(device);
+    if (comm) ncclCommDestroy(comm);
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk})
+      if (p) (void)hipFree(p);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  uint64_t n_features() const override { return nf; }
+  uint64_t n_samples() const override { return n_total; }
+  uint64_t n_local() const override { return n_local_; }
+
+  double* ensure(double*& p, size_t& cap, size_t n) {
+    if (n > cap) {
+      if (p) HIP_OK(hipFree(p));
+      HIP_OK(hipMalloc(&p, n * sizeof(double)));
+      cap = n;
+    }
+    return p;
+  }
+
+  void alloc_x(uint64_t nf_, uint64_t n_local, uint64_t n_tot, uint64_t t0_) {
+    HIP_OK(hipSetDevice(device));
+    if (X) HIP_OK(hipFree(X));
+    nf = nf_; n_local_ = n_local; n_total = n_tot; t0 = t0_;
+    ldx = (n_local + 15) / 16 * 16;
+    if (ldx == 0) ldx = 16;
+    HIP_OK(hipMalloc(&X, nf * ldx * sizeof(double) + 256));
+    HIP_OK(hipMemsetAsync(X, 0, nf * ldx * sizeof(double) + 256, stream));
+  }
+
+  void load(const double* xh, uint64_t nf_, uint64_t n_local, uint64_t n_tot, uint64_t t0_) {
+    alloc_x(nf_, n_local, n_tot, t0_);
+    if (n_local)
+      HIP_OK(hipMemcpy2DAsync(X, ldx * sizeof(double), xh, n_local * sizeof(double), n_local * sizeof(double),
+                              nf, hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  void download(double* out) {
+    HIP_OK(hipSetDevice(device));
+    if (n_local_)
+      HIP_OK(hipMemcpy2DAsync(out, n_local_ * sizeof(double), X, ldx * sizeof(double), n_local_ * sizeof(double),
+                              nf, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  static uint64_t shard_t0(uint64_t n_tot, int world, int rank) {
+    const uint64_t base = n_tot / world, rem = n_tot % world;
+    return rank * base + std::min<uint64_t>(rank, rem);
+  }
+  static uint64_t shard_n(uint64_t n_tot, int world, int rank) {
+    const uint64_t base = n_tot / world, rem = n_tot % world;
+    return base + (rank < (int)rem ? 1 : 0);
+  }
+
+  void generate(uint64_t nf_, uint64_t n_tot, uint64_t seed, double* a_out) {
+    const uint64_t tt0 = shard_t0(n_tot, world, rank), nl = shard_n(n_tot, world, rank);
+    alloc_x(nf_, nl, n_tot, tt0);
+    // mixing matrix: states N·T + 1 … N·T + N² (benchmarks.rs:26-32)
+    std::vector<double> A(nf * nf);
+    const Affine j = lcg_jump(nf * n_tot);
+    uint64_t st = j.a * seed + j.c;
+    for (size_t e = 0; e < nf * nf; ++e) {
+      st = st * 6364136223846793005ull + 1ull;
+      A[e] = (double)(st >> 33) / 2147483648.0 - 0.5;
+    }
+    if (a_out) std::memcpy(a_out, A.data(), A.size() * sizeof(double));
+    double* dA = ensure(d_w, cap_w, nf * nf);
+    HIP_OK(hipMemcpyAsync(dA, A.data(), A.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    const Affine jt = lcg_jump(n_tot);  // row i → i+1 at fixed t
+    const uint64_t CH = 1ull << 20;
+    double* S = ensure(d_chunk, cap_chunk, nf * CH);
+    for (uint64_t c0 = 0; c0 < nl; c0 += CH) {
+      const uint64_t cn = std::min<uint64_t>(CH, nl - c0);
+      k_gen_sources<<<(cn + 255) / 256, 256, 0, stream>>>(S, CH, (int)nf, tt0 + c0, cn, seed, jt.a, jt.c);
+      HIP_OK(hipGetLastError());
+      // X[:, c0:c0+cn] = A·S (benchmarks.rs:34)
+      k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(S, CH, cn, (int)nf, (int)nf, dA, nullptr, 0.0, 0, cn,
+                                                               X + c0, ldx, nullptr, nullptr, nullptr, 0);
+      HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  void allreduce(double* d, size_t n) {
+    if (world > 1) RCCL_OK(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm, stream));
+  }
+
+  void rowsum(double* out) override {
+    HIP_OK(hipSetDevice(device));
+    const int nwg = n_cu;
+    const uint64_t per = (n_local_ + nwg - 1) / nwg;
+    double* part = ensure(d_part, cap_part, (size_t)nwg * nf);
+    double* st = ensure(d_stats, cap_stats, nf);
+    k_rowsum<<<nwg, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, per, part);
+    HIP_OK(hipGetLastError());
+    k_sum_slabs<<<(nf + 255) / 256, 256, 0, stream>>>(part, nwg, nf, st);
+    allreduce(st, nf);
+    HIP_OK(hipMemcpyAsync(out, st, nf * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  void gram(const double* mu, double* out) override {
+    std::vector<double> eye(nf * nf, 0.0);
+    for (size_t i = 0; i < nf; ++i) eye[i * nf + i] = 1.0;
+    std::vector<double> st(EvalStats::size(nf, false));
+    run_eval(eye.data(), nf, mu, DENS_LINEAR, 1.0, false, st.data());
+    std::memcpy(out, st.data(), nf * nf * sizeof(double));
+  }
+
+  void eval(const double* w, size_t nc, const double* mu, pc_density d, bool need_h, EvalStats* out) override {
+    out->nc = nc;
+    out->has_h = need_h;
+    out->buf.assign(EvalStats::size(nc, need_h), 0.0);
+    run_eval(w, nc, mu, d.kind, d.alpha, need_h, out->buf.data());
+  }
+
+  static int pick_nb(size_t nc) { return nc <= 16 ? 1 : nc <= 32 ? 2 : nc <= 64 ? 4 : nc <= 128 ? 8 : 0; }
+
+  template <int NB, bool H, int D>
+  void launch_fused(int nfp, const double* dmu, double alpha, double* st, size_t nc) {
+    using S = FusedShape<NB>;
+    const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
+    int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_blocks, 1));
+    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
+    nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    const size_t pstride = fused_partial_stride(S::NCP, H);
+    double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
+    const size_t lds = (size_t)(S::TS * nfp * 16 + (H ? 3 : 2) * S::FRAGS) * sizeof(double);
+    auto kern = k_eval_fused<NB, H, D>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr_set = true;
+    }
+    HIP_OK(hipEventRecord(ev[1], stream));
+    kern<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, nfp, d_w, dmu, alpha, bpw, n_blocks, part);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    const size_t total = EvalStats::size(nc, H);
+    k_reduce<<<(total + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st);
+    HIP_OK(hipGetLastError());
+  }
+
+  template <int NB, bool H>
+  void dispatch_dens(int dens, int nfp, const double* dmu, double alpha, double* st, size_t nc) {
+    switch (dens) {
+      case DENS_TANH: launch_fused<NB, H, DENS_TANH>(nfp, dmu, alpha, st, nc); break;
+      case DENS_EXP: launch_fused<NB, H, DENS_EXP>(nfp, dmu, alpha, st, nc); break;
+      case DENS_CUBE: launch_fused<NB, H, DENS_CUBE>(nfp, dmu, alpha, st, nc); break;
+      default: launch_fused<NB, H, DENS_LINEAR>(nfp, dmu, alpha, st, nc); break;
+    }
+  }
+  template <int NB>
+  void dispatch_h(bool h, int dens, int nfp, const double* dmu, double alpha, double* st, size_t nc) {
+    if (h) dispatch_dens<NB, true>(dens, nfp, dmu, alpha, st, nc);
+    else dispatch_dens<NB, false>(dens, nfp, dmu, alpha, st, nc);
+  }
+
+  void run_eval(const double* w, size_t nc, const double* mu, int dens, double alpha, bool need_h, double* stats_host) {
+    HIP_OK(hipSetDevice(device));
+    const size_t total = EvalStats::size(nc, need_h);
+    double* st = ensure(d_stats, cap_stats, total);
+    HIP_OK(hipEventRecord(ev[0], stream));
+    const int nb = pick_nb(nc);
+    const int nfp = (int)((nf + 3) / 4 * 4);
+    const bool fused = nb > 0 && nfp <= 4 * KSMAX && (8 / nb) * nfp <= 128 && !(need_h && nb == 8);
+    double* dmu = nullptr;
+    if (mu) {
+      dmu = ensure(d_mu, cap_mu, std::max<size_t>(nfp, nf));
+      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    }
+    if (fused) {
+      const int ncp = 16 * nb;
+      std::vector<double> wp((size_t)ncp * nfp, 0.0);
+      for (size_t i = 0; i < nc; ++i)
+        for (size_t k = 0; k < nf; ++k) wp[i * nfp + k] = w[i * nf + k];
+      ensure(d_w, cap_w, wp.size());
+      HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+      switch (nb) {
+        case 1: dispatch_h<1>(need_h, dens, nfp, dmu, alpha, st, nc); break;
+        case 2: dispatch_h<2>(need_h, dens, nfp, dmu, alpha, st, nc); break;
+        case 4: dispatch_h<4>(need_h, dens, nfp, dmu, alpha, st, nc); break;
+        default: dispatch_h<8>(need_h, dens, nfp, dmu, alpha, st, nc); break;
+      }
+    } else {
+      generic_eval(w, nc, dmu, dens, alpha, need_h, st);
+    }
+    allreduce(st, total);
+    HIP_OK(hipMemcpyAsync(stats_host, st, total * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipEventRecord(ev[3], stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    float a = 0, b = 0;
+    if (fused) { HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2])); }
+    HIP_OK(hipEventElapsedTime(&b, ev[0], ev[3]));
+    last_kernel_ms = fused ? a : b;
+    last_call_ms = b;
+  }
+
+  void generic_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st) {
+    const uint64_t CH = 1ull << 16;
+    const int splits = 16;
+    const size_t nsq = nc * nc;
+    double* dw = ensure(d_w, cap_w, nc * nf);
+    HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    // chunk scratch: Y, ψ, ψ′, ℓ (nc × CH each) + slabs + row sums
+    const size_t need = 4 * nc * CH + (need_h ? 2 : 1) * splits * nsq + 3 * nc;
+    double* base = ensure(d_chunk, cap_chunk, need);
+    double *Y = base, *P = Y + nc * CH, *D = P + nc * CH, *L = D + nc * CH;
+    double* gsl = L + nc * CH;
+    double* hsl = gsl + splits * nsq;
+    double* rs = hsl + (need_h ? splits * nsq : 0);
+    HIP_OK(hipMemsetAsync(gsl, 0, ((need_h ? 2 : 1) * splits * nsq + 3 * nc) * sizeof(double), stream));
+    const int tiles = (int)((nc + 63) / 64);
+    for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
+      const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
+      const uint64_t g = (cn + 255) / 256;
+      switch (dens) {
+        case DENS_TANH: k_ycomp<DENS_TANH><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
+        case DENS_EXP: k_ycomp<DENS_EXP><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
+        case DENS_CUBE: k_ycomp<DENS_CUBE><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
+        default: k_ycomp<DENS_LINEAR><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
+      }
+      HIP_OK(hipGetLastError());
+      k_gemm_nt<false><<<tiles * tiles * splits, 256, 0, stream>>>(P, Y, CH, (int)nc, cn, splits, gsl);
+      if (need_h) k_gemm_nt<true><<<tiles * tiles * splits, 256, 0, stream>>>(D, Y, CH, (int)nc, cn, splits, hsl);
+      k_rowsums_chunk<<<dim3((unsigned)nc, 3), 256, 0, stream>>>(D, L, Y, CH, CH, cn, cn, rs, (int)nc);
+      HIP_OK(hipGetLastError());
+    }
+    k_sum_slabs<<<(nsq + 255) / 256, 256, 0, stream>>>(gsl, splits, nsq, st);
+    if (need_h) k_sum_slabs<<<(nsq + 255) / 256, 256, 0, stream>>>(hsl, splits, nsq, st + nsq);
+    HIP_OK(hipMemcpyAsync(st + (need_h ? 2 : 1) * nsq, rs, 3 * nc * sizeof(double), hipMemcpyDeviceToDevice, stream));
+    HIP_OK(hipGetLastError());
+  }
+
+  void sources(const double* w, size_t nc, const double* mu, double* out) override {
+    HIP_OK(hipSetDevice(device));
+    double* dw = ensure(d_w, cap_w, nc * nf);
+    HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    double* dmu = nullptr;
+    if (mu) {
+      dmu = ensure(d_mu, cap_mu, nf);
+      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    }
+    const uint64_t CH = 1ull << 20;
+    double* Y = ensure(d_chunk, cap_chunk, nc * CH);
+    for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
+      const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
+      k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, 0.0, c0,
+                                                               cn, Y, CH, nullptr, nullptr, nullptr, 0);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpy2DAsync(out + c0, n_local_ * sizeof(double), Y, CH * sizeof(double), cn * sizeof(double), nc,
+                              hipMemcpyDeviceToHost, stream));
+    }
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  void moments4(const double* w, size_t nc, const double* mu, double* out) override {
+    HIP_OK(hipSetDevice(device));
+    const int np = (int)(nc * (nc + 1) / 2);
+    std::vector<int> pi(np), pj(np);
+    {
+      int q = 0;
+      for (int i = 0; i < (int)nc; ++i)
+        for (int j = i; j < (int)nc; ++j) { pi[q] = i; pj[q] = j; ++q; }
+    }
+    double* dw = ensure(d_w, cap_w, nc * nf);
+    HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    double* dmu = nullptr;
+    if (mu) {
+      dmu = ensure(d_mu, cap_mu, nf);
+      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    }
+    const uint64_t CH = 1ull << 16;
+    const size_t need = nc * CH + (size_t)np * np + 2 * (size_t)np;
+    double* Y = ensure(d_chunk, cap_chunk, need);
+    double* acc = Y + nc * CH;
+    int* dpi = reinterpret_cast<int*>(acc + (size_t)np * np);
+    int* dpj = dpi + np;
+    HIP_OK(hipMemcpyAsync(dpi, pi.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dpj, pj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemsetAsync(acc, 0, (size_t)np * np * sizeof(double), stream));
+    const int tiles = (np + 31) / 32;
+    for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
+      const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
+      k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, 0.0, c0,
+                                                               cn, Y, CH, nullptr, nullptr, nullptr, 0);
+      k_moments4<<<tiles * tiles, 256, 0, stream>>>(Y, CH, cn, (int)nc, dpi, dpj, np, acc);
+      HIP_OK(hipGetLastError());
+    }
+    allreduce(acc, (size_t)np * np);
+    HIP_OK(hipMemcpyAsync(out, acc, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    for (int p = 0; p < np; ++p)  // mirror the upper tiles
+      for (int q = 0; q < p; ++q) out[(size_t)p * np + q] = out[(size_t)q * np + p];
+  }
+};
+
+// factory + thin accessors used by capi.cpp
+Evaluator* make_device_ctx(int device, int rank, int world, const char* uid) {
+  return new DeviceCtx(device, rank, world, uid);
+}
+void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0) {
+  static_cast<DeviceCtx*>(e)->load(x, nf, nl, nt, t0);
+}
+void device_ctx_generate(Evaluator* e, uint64_t nf, uint64_t nt, uint64_t seed, double* a_out) {
+  static_cast<DeviceCtx*>(e)->generate(nf, nt, seed, a_out);
+}
+void device_ctx_download(Evaluator* e, double* out) { static_cast<DeviceCtx*>(e)->download(out); }
+uint64_t device_ctx_t0(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->t0; }
+void device_ctx_timing(const Evaluator* e, double* k, double* c) {
+  auto* d = static_cast<const DeviceCtx*>(e);
+  *k = d->last_kernel_ms;
+  *c = d->last_call_ms;
+}
+void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double* mu, int dens, double alpha,
+                         bool need_h, double* stats) {
+  static_cast<DeviceCtx*>(e)->run_eval(w, nc, mu, dens, alpha, need_h, stats);
+}
+int rccl_unique_id(char* out) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return 1;
+  std::memcpy(out, &id, sizeof id);
+  return 0;
+}
+
+}  // namespace pcamd

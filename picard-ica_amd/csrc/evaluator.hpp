@@ -1,0 +1,62 @@
+// The operator boundary between the host Picard driver and the device.
+// Everything the reference computes over the full N×T data
+// (src/core.rs:215-274, :39-85; src/whitening.rs:24-116; src/jade.rs:91-113)
+// is one of these calls; everything else is N×N host work.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/picard_mi355x.h"
+
+namespace pcamd {
+
+// src/error.rs:9-42 as an exception carrying the pc_status code and the
+// Display text of src/error.rs:44-74.
+struct PicardError : std::runtime_error {
+  int code;
+  PicardError(int c, const std::string& msg) : std::runtime_error(msg), code(c) {}
+};
+inline PicardError invalid_dimensions(const std::string& m) {
+  return PicardError(PC_ERR_INVALID_DIMENSIONS, "Invalid dimensions: " + m);
+}
+inline PicardError singular_matrix() {
+  return PicardError(PC_ERR_SINGULAR_MATRIX, "Singular matrix encountered during computation");
+}
+inline PicardError computation_error(const std::string& m) {
+  return PicardError(PC_ERR_COMPUTATION, "Computation error: " + m);
+}
+inline PicardError invalid_config(const std::string& p, const std::string& m) {
+  return PicardError(PC_ERR_INVALID_CONFIG, "Invalid configuration for '" + p + "': " + m);
+}
+
+// Packed statistics of one fused pass (see pc_ctx_eval).
+struct EvalStats {
+  size_t nc = 0;
+  bool has_h = false;
+  std::vector<double> buf;
+  const double* G() const { return buf.data(); }
+  const double* H() const { return buf.data() + nc * nc; }
+  const double* dpsi() const { return buf.data() + (has_h ? 2 : 1) * nc * nc; }
+  const double* ll() const { return dpsi() + nc; }
+  const double* y2() const { return dpsi() + 2 * nc; }
+  static size_t size(size_t nc, bool h) { return (h ? 2 : 1) * nc * nc + 3 * nc; }
+};
+
+class Evaluator {
+ public:
+  virtual ~Evaluator() = default;
+  virtual uint64_t n_features() const = 0;
+  virtual uint64_t n_samples() const = 0;  // global T over all ranks
+  virtual void rowsum(double* out) = 0;
+  virtual void gram(const double* mu, double* out) = 0;
+  virtual void eval(const double* w, size_t nc, const double* mu, pc_density d, bool need_h,
+                    EvalStats* out) = 0;
+  // this rank's shard of Y = W·(X−μ) (nc × n_local)
+  virtual void sources(const double* w, size_t nc, const double* mu, double* out) = 0;
+  virtual uint64_t n_local() const = 0;
+  virtual void moments4(const double* w, size_t nc, const double* mu, double* out) = 0;
+};
+
+}  // namespace pcamd

@@ -1,0 +1,224 @@
+// Host N×N linear algebra; see host_linalg.hpp.
+#include "host_linalg.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+
+namespace pcamd {
+
+Mat matmul(const Mat& a, const Mat& b) {
+  Mat c(a.rows, b.cols);
+  const size_t n = a.rows, k = a.cols, m = b.cols;
+  const double* A = a.data();
+  const double* B = b.data();
+  double* C = c.data();
+  // i-k-j order: contiguous inner loop over the output row; rows in parallel.
+#pragma omp parallel for schedule(static) if (n * k * m > (1u << 18))
+  for (long i = 0; i < (long)n; ++i) {
+    double* ci = C + (size_t)i * m;
+    for (size_t p = 0; p < k; ++p) {
+      const double aip = A[(size_t)i * k + p];
+      const double* bp = B + p * m;
+#pragma omp simd
+      for (size_t j = 0; j < m; ++j) ci[j] += aip * bp[j];
+    }
+  }
+  return c;
+}
+
+Mat transpose(const Mat& a) {
+  Mat t(a.cols, a.rows);
+  for (size_t i = 0; i < a.rows; ++i)
+    for (size_t j = 0; j < a.cols; ++j) t(j, i) = a(i, j);
+  return t;
+}
+
+Mat matmul_nt(const Mat& a, const Mat& b) { return matmul(a, transpose(b)); }
+
+Mat add(const Mat& a, const Mat& b) {
+  Mat c = a;
+  for (size_t i = 0; i < c.a.size(); ++i) c.a[i] += b.a[i];
+  return c;
+}
+
+Mat sub(const Mat& a, const Mat& b) {
+  Mat c = a;
+  for (size_t i = 0; i < c.a.size(); ++i) c.a[i] -= b.a[i];
+  return c;
+}
+
+Mat scale(const Mat& a, double s) {
+  Mat c = a;
+  for (double& v : c.a) v *= s;
+  return c;
+}
+
+double max_abs(const Mat& a) {
+  // fold(0.0, f64::max): NaN entries are skipped by f64::max (core.rs:289)
+  double m = 0.0;
+  for (double v : a.a) m = std::fmax(m, std::fabs(v));
+  return m;
+}
+
+double dot_sum(const Mat& a, const Mat& b) {
+  double s = 0.0;
+  for (size_t i = 0; i < a.a.size(); ++i) s += a.a[i] * b.a[i];
+  return s;
+}
+
+void eigh(const Mat& s_in, std::vector<double>* vals, Mat* vecs) {
+  const size_t n = s_in.rows;
+  Mat a = s_in;
+  // symmetrise from the lower triangle (UPLO::Lower, math.rs:16)
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = i + 1; j < n; ++j) a(i, j) = a(j, i);
+  Mat v = Mat::eye(n);
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    double off = 0.0, diag = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+      diag += a(i, i) * a(i, i);
+      for (size_t j = i + 1; j < n; ++j) off += a(i, j) * a(i, j);
+    }
+    if (off <= 1e-32 * diag || off == 0.0) break;
+    for (size_t p = 0; p < n; ++p) {
+      for (size_t q = p + 1; q < n; ++q) {
+        const double apq = a(p, q);
+        if (apq == 0.0) continue;
+        const double app = a(p, p), aqq = a(q, q);
+        if (std::fabs(apq) < 1e-300) { a(p, q) = a(q, p) = 0.0; continue; }
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0);
+        const double sn = t * c;
+        for (size_t k = 0; k < n; ++k) {
+          const double akp = a(k, p), akq = a(k, q);
+          a(k, p) = c * akp - sn * akq;
+          a(k, q) = sn * akp + c * akq;
+        }
+        for (size_t k = 0; k < n; ++k) {
+          const double apk = a(p, k), aqk = a(q, k);
+          a(p, k) = c * apk - sn * aqk;
+          a(q, k) = sn * apk + c * aqk;
+        }
+        a(p, q) = a(q, p) = 0.0;
+        for (size_t k = 0; k < n; ++k) {
+          const double vkp = v(k, p), vkq = v(k, q);
+          v(k, p) = c * vkp - sn * vkq;
+          v(k, q) = sn * vkp + c * vkq;
+        }
+      }
+    }
+  }
+  std::vector<size_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return a(x, x) < a(y, y); });
+  vals->assign(n, 0.0);
+  *vecs = Mat(n, n);
+  for (size_t c = 0; c < n; ++c) {
+    (*vals)[c] = a(order[c], order[c]);
+    for (size_t r = 0; r < n; ++r) (*vecs)(r, c) = v(r, order[c]);
+  }
+}
+
+bool sym_decorrelation(const Mat& w, Mat* out) {
+  Mat ww_t = matmul_nt(w, w);
+  std::vector<double> ev;
+  Mat u;
+  eigh(ww_t, &ev, &u);
+  double mn = std::numeric_limits<double>::infinity();
+  for (double e : ev) mn = std::fmin(mn, e);
+  if (mn < 1e-10) return false;
+  Mat scaled = u;
+  for (size_t r = 0; r < u.rows; ++r)
+    for (size_t c = 0; c < u.cols; ++c) scaled(r, c) *= 1.0 / std::sqrt(ev[c]);
+  *out = matmul(matmul_nt(scaled, u), w);
+  return true;
+}
+
+Mat matrix_exp(const Mat& a) {
+  const size_t n = a.rows;
+  const double norm = max_abs(a);
+  if (norm < 1e-15) return Mat::eye(n);
+  const int s = (int)std::fmax(std::ceil(std::log2(norm)), 0.0);
+  const double sc = std::ldexp(1.0, s);
+  Mat as = a;
+  for (double& v : as.a) v /= sc;
+  Mat result = Mat::eye(n), term = Mat::eye(n);
+  for (int k = 1; k <= 30; ++k) {
+    term = matmul(term, as);
+    for (double& v : term.a) v /= (double)k;
+    for (size_t i = 0; i < result.a.size(); ++i) result.a[i] += term.a[i];
+    if (max_abs(term) < 1e-16) break;
+  }
+  for (int i = 0; i < s; ++i) result = matmul(result, result);
+  return result;
+}
+
+void sln_det(const Mat& m, double* sign, double* logabs) {
+  const size_t n = m.rows;
+  Mat lu = m;
+  double sg = 1.0, la = 0.0;
+  for (size_t k = 0; k < n; ++k) {
+    size_t piv = k;
+    double best = std::fabs(lu(k, k));
+    for (size_t i = k + 1; i < n; ++i)
+      if (std::fabs(lu(i, k)) > best) { best = std::fabs(lu(i, k)); piv = i; }
+    if (best == 0.0) { *sign = 0.0; *logabs = -std::numeric_limits<double>::infinity(); return; }
+    if (piv != k) {
+      for (size_t j = 0; j < n; ++j) std::swap(lu(k, j), lu(piv, j));
+      sg = -sg;
+    }
+    const double d = lu(k, k);
+    for (size_t i = k + 1; i < n; ++i) {
+      const double f = lu(i, k) / d;
+      lu(i, k) = f;
+      for (size_t j = k + 1; j < n; ++j) lu(i, j) -= f * lu(k, j);
+    }
+  }
+  for (size_t k = 0; k < n; ++k) {
+    const double d = lu(k, k);
+    if (d < 0) sg = -sg;
+    la += std::log(std::fabs(d));
+  }
+  *sign = sg;
+  *logabs = la;
+}
+
+Mat skew_symmetric(const Mat& a) {
+  Mat r(a.rows, a.cols);
+  for (size_t i = 0; i < a.rows; ++i)
+    for (size_t j = 0; j < a.cols; ++j) r(i, j) = (a(i, j) - a(j, i)) / 2.0;
+  return r;
+}
+
+bool invert_matrix(const Mat& m, Mat* out) {
+  const size_t n = m.rows;
+  if (n != m.cols) return false;
+  Mat aug(n, 2 * n);
+  for (size_t i = 0; i < n; ++i) {
+    for (size_t j = 0; j < n; ++j) aug(i, j) = m(i, j);
+    aug(i, n + i) = 1.0;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    size_t max_row = i;
+    for (size_t k = i + 1; k < n; ++k)
+      if (std::fabs(aug(k, i)) > std::fabs(aug(max_row, i))) max_row = k;
+    for (size_t j = 0; j < 2 * n; ++j) std::swap(aug(i, j), aug(max_row, j));
+    if (std::fabs(aug(i, i)) < 1e-15) return false;
+    const double pivot = aug(i, i);
+    for (size_t j = 0; j < 2 * n; ++j) aug(i, j) /= pivot;
+    for (size_t k = 0; k < n; ++k) {
+      if (k == i) continue;
+      const double f = aug(k, i);
+      for (size_t j = 0; j < 2 * n; ++j) aug(k, j) -= f * aug(i, j);
+    }
+  }
+  *out = Mat(n, n);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) (*out)(i, j) = aug(i, n + j);
+  return true;
+}
+
+}  // namespace pcamd

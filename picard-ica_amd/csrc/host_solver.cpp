@@ -1,0 +1,551 @@
+// Host Picard driver over an Evaluator. Statement order follows the
+// reference so that the host-side N×N arithmetic is the reference's:
+//   src/solver.rs:45-189 (fit_with_config), :218-249 (ica_par)
+//   src/core.rs:39-96 (compute_loss), :99-150 (line_search), :162-401 (run)
+//   src/lbfgs.rs:84-171, src/whitening.rs:48-107, src/jade.rs:22-197
+// Every N×T quantity comes from the Evaluator (one fused device pass).
+#include "host_solver.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+
+namespace pcamd {
+
+std::string rust_e4(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "inf" : "-inf";
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%.4e", v);
+  std::string s(buf);
+  size_t e = s.find('e');
+  int ex = std::atoi(s.c_str() + e + 1);
+  return s.substr(0, e) + "e" + std::to_string(ex);
+}
+
+// ---------------------------------------------------------------- lbfgs.rs
+Mat compute_direction(const Mat& g, const Mat& h, const std::vector<double>& h_off,
+                      const LbfgsMemory& mem, bool ortho) {
+  Mat q = g;
+  const size_t k = mem.len();
+  std::vector<double> alpha_list(k);
+  for (size_t ii = k; ii-- > 0;) {  // .rev()
+    const double alpha = mem.r_list[ii] * dot_sum(mem.s_list[ii], q);
+    alpha_list[ii] = alpha;
+    const Mat& y = mem.y_list[ii];
+    for (size_t e = 0; e < q.a.size(); ++e) q.a[e] = q.a[e] - alpha * y.a[e];
+  }
+  Mat z;
+  if (ortho) {
+    Mat zq(q.rows, q.cols);
+    for (size_t e = 0; e < q.a.size(); ++e) zq.a[e] = q.a[e] / h.a[e];
+    z = Mat(q.rows, q.cols);
+    for (size_t i = 0; i < q.rows; ++i)
+      for (size_t j = 0; j < q.cols; ++j) z(i, j) = (zq(i, j) - zq(j, i)) / 2.0;
+  } else {
+    z = solve_hessian_system(h, h_off, q);
+  }
+  for (size_t ii = 0; ii < k; ++ii) {
+    const double beta = mem.r_list[ii] * dot_sum(mem.y_list[ii], z);
+    const Mat& s = mem.s_list[ii];
+    const double f = alpha_list[ii] - beta;
+    for (size_t e = 0; e < z.a.size(); ++e) z.a[e] = z.a[e] + f * s.a[e];
+  }
+  for (double& v : z.a) v = -v;
+  return z;
+}
+
+Mat solve_hessian_system(const Mat& h, const std::vector<double>& h_off, const Mat& g) {
+  const size_t n = h.rows;
+  Mat r(n, n);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) {
+      const double det = h(i, j) * h(j, i) - h_off[i] * h_off[j];
+      if (std::fabs(det) > 1e-15) r(i, j) = (h(j, i) * g(i, j) - h_off[i] * g(j, i)) / det;
+    }
+  return r;
+}
+
+void regularize_hessian(Mat& h, const std::vector<double>& h_off, double lambda_min) {
+  const size_t n = h.rows;
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j) {
+      if (i == j) continue;
+      const double diff = h(i, j) - h(j, i);
+      const double discr = std::sqrt(diff * diff + 4.0 * h_off[i] * h_off[j]);
+      const double eig = 0.5 * (h(i, j) + h(j, i) - discr);
+      if (eig < lambda_min) h(i, j) += lambda_min - eig;
+    }
+}
+
+// ---------------------------------------------------------- rng (w_init)
+// rand 0.9.2 StdRng/ChaCha12 + rand_distr ziggurat are not reproducible
+// offline; a seeded SplitMix64 + Box–Muller stands in. Runs
+// that need reference bit-parity pass an explicit w_init.
+namespace {
+struct SplitMix {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  double uniform() { return ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
+};
+}  // namespace
+
+// ------------------------------------------------------------- Solver
+Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
+  // config.rs:104-142
+  if (cfg.max_iter == 0) throw invalid_config("max_iter", "must be greater than 0");
+  if (!(cfg.tol > 0.0)) throw invalid_config("tol", "must be positive");
+  if (!(cfg.lambda_min > 0.0)) throw invalid_config("lambda_min", "must be positive");
+  if (cfg.m == 0) throw invalid_config("m", "L-BFGS memory size must be at least 1");
+  if (cfg.has_fastica_it && cfg.has_jade_it)
+    throw invalid_config("jade_it", "cannot use both fastica_it and jade_it; choose one warm start method");
+  if (cfg.density.kind < PC_DENSITY_TANH || cfg.density.kind > PC_DENSITY_CUBE)
+    throw invalid_config("density", "unknown density kind");
+  if (cfg.w_init) {
+    w_init_user_.assign(cfg.w_init, cfg.w_init + cfg.w_init_rows * cfg.w_init_cols);
+    cfg_.w_init = nullptr;
+  }
+  nf_ = ev->n_features();
+  T_ = ev->n_samples();
+  const uint64_t n = nf_, p = T_;
+  if (n == 0 || p == 0) throw invalid_dimensions("Input matrix cannot be empty");  // solver.rs:50-54
+
+  SplitMix rng{cfg.has_random_state ? cfg.random_state : (uint64_t)std::random_device{}() << 32 ^ std::random_device{}()};
+  const uint64_t mn = n < p ? n : p;
+  uint64_t ncomp = cfg.has_n_components ? cfg.n_components : mn;
+  if (ncomp > mn) ncomp = mn;  // solver.rs:63
+  extended_ = cfg.has_extended ? (cfg.extended != 0) : (cfg.ortho != 0);  // config.rs:99-101
+  if (cfg.density.kind != PC_DENSITY_TANH && extended_ && !cfg.ortho)  // solver.rs:69-74
+    std::fprintf(stderr,
+                 "Warning: Using a density other than tanh with extended=true and ortho=false "
+                 "may result in incorrect estimation or numerical overflow\n");
+  const double pf = (double)p;
+  // center: whitening.rs:24-35 (μ folded into every pass; X is never copied)
+  if (cfg.centering) {
+    mu_.assign(n, 0.0);
+    ev->rowsum(mu_.data());
+    for (double& v : mu_) v /= pf;
+    has_mu_ = true;
+  }
+  const double* mu = has_mu_ ? mu_.data() : nullptr;
+  // whiten: whitening.rs:48-116 via the Gram X·Xᵀ = U S² Uᵀ
+  if (cfg.whiten) {
+    if (ncomp > n) {
+      throw invalid_dimensions("n_components (" + std::to_string(ncomp) +
+                               ") cannot exceed n_features (" + std::to_string(n) + ")");
+    }
+    gram_ = Mat(n, n);
+    ev->gram(mu, gram_.data());
+    has_gram_ = true;
+    std::vector<double> lam;
+    Mat u;
+    eigh(gram_, &lam, &u);
+    // descending singular values s_i = sqrt(λ), columns of U in that order
+    std::vector<double> s(n);
+    Mat ud(n, n);
+    for (size_t c = 0; c < n; ++c) {
+      const size_t src = n - 1 - c;
+      s[c] = std::sqrt(std::fmax(lam[src], 0.0));
+      for (size_t r = 0; r < n; ++r) ud(r, c) = u(r, src);
+    }
+    double min_sv = std::numeric_limits<double>::infinity();
+    for (size_t i = 0; i < ncomp; ++i) min_sv = std::fmin(min_sv, s[i]);
+    if (min_sv < 1e-10) throw singular_matrix();  // whitening.rs:72-79
+    const double sc = std::sqrt(pf);
+    K_ = Mat(ncomp, n);
+    for (size_t i = 0; i < ncomp; ++i)
+      for (size_t j = 0; j < n; ++j) K_(i, j) = ud(j, i) / s[i] * sc;
+    for (size_t i = 0; i < ncomp; ++i) {  // whitening.rs:93-107 (max_by keeps the last max)
+      size_t mi = 0;
+      double best = -1.0;
+      for (size_t j = 0; j < n; ++j)
+        if (std::fabs(K_(i, j)) >= best) { best = std::fabs(K_(i, j)); mi = j; }
+      if (K_(i, mi) < 0.0)
+        for (size_t j = 0; j < n; ++j) K_(i, j) = -K_(i, j);
+    }
+    has_k_ = true;
+  }
+  nc_ = has_k_ ? ncomp : n;  // solver.rs:95
+  // w_init: solver.rs:98-121
+  if (cfg.w_init != nullptr) {
+    if (cfg.w_init_rows != nc_ || cfg.w_init_cols != nc_)
+      throw invalid_dimensions("w_init shape [" + std::to_string(cfg.w_init_rows) + ", " +
+                               std::to_string(cfg.w_init_cols) + "] doesn't match expected (" +
+                               std::to_string(nc_) + ", " + std::to_string(nc_) + ")");
+    w_init_ = Mat(nc_, nc_);
+    w_init_.a = w_init_user_;
+  } else {
+    Mat w(nc_, nc_);
+    for (size_t i = 0; i < nc_ * nc_; i += 2) {
+      const double u1 = rng.uniform(), u2 = rng.uniform();
+      const double r = std::sqrt(-2.0 * std::log(u1));
+      w.a[i] = r * std::cos(2.0 * M_PI * u2);
+      if (i + 1 < nc_ * nc_) w.a[i + 1] = r * std::sin(2.0 * M_PI * u2);
+    }
+    if (!sym_decorrelation(w, &w_init_)) throw singular_matrix();
+  }
+  // warm starts: solver.rs:124-137
+  if (cfg.has_jade_it) {
+    if (cfg.verbose) std::printf("Running %llu iterations of JADE...\n", (unsigned long long)cfg.jade_it);
+    w_init_ = jade(cfg.jade_it, 1e-6);
+  } else if (cfg.has_fastica_it) {
+    if (cfg.verbose) std::printf("Running %llu iterations of FastICA...\n", (unsigned long long)cfg.fastica_it);
+    w_init_ = ica_par(w_init_);
+  }
+  // x1 = w_init·x1 (solver.rs:140), kept as the composed map P
+  P_ = has_k_ ? matmul(w_init_, K_) : w_init_;
+  has_cov_ = extended_ && cfg.whiten;  // solver.rs:143-147
+  if (cfg.verbose) std::printf("Running Picard...\n");
+  init_core();
+}
+
+void Solver::evaluate(const Mat& w_core, EvalStats* out) {
+  Mat wt = matmul(w_core, P_);
+  ev_->eval(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
+  ++last_evals_;
+  ++total_evals_;
+}
+
+// core.rs:39-85 + loss_to_f64 core.rs:90-96, from the pass's per-row sums
+double Solver::loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular) {
+  const double t = (double)T_;
+  const bool ortho = cfg_.ortho != 0;
+  double loss = 0.0;
+  *singular = false;
+  if (!ortho) {
+    double sg, la;
+    sln_det(w, &sg, &la);
+    if (sg == 0.0) { *singular = true; return 1e15; }
+    loss = -la;
+  }
+  const double* ll = s.ll();
+  const double* y2 = s.y2();
+  for (size_t i = 0; i < nc_; ++i) {
+    loss += signs[i] * ll[i] / t;
+    if (extended_ && !ortho) loss += 0.5 * y2[i] / t;
+  }
+  return loss;
+}
+
+void Solver::init_core() {  // core.rs:175-209
+  const size_t n = nc_;
+  W_ = Mat::eye(n);
+  signs_.assign(n, 1.0);
+  old_signs_ = signs_;
+  last_evals_ = 0;
+  evaluate(W_, &S_);
+  bool singular;
+  current_loss_ = loss_of(S_, W_, signs_, &singular);
+  if (singular) throw singular_matrix();
+  gradient_norm_ = 1.0;
+  converged_ = false;
+  if (extended_) {
+    if (has_cov_) {
+      C_ = Mat::eye(n);
+    } else {  // Y·Yᵀ/T of x1 = P·(X−μ): P·Gram·Pᵀ/T (core.rs:202)
+      if (!has_gram_) {
+        gram_ = Mat(nf_, nf_);
+        ev_->gram(has_mu_ ? mu_.data() : nullptr, gram_.data());
+        has_gram_ = true;
+      }
+      C_ = matmul_nt(matmul(P_, gram_), P_);
+      for (double& v : C_.a) v /= (double)T_;
+    }
+  } else {
+    C_ = Mat::eye(n);
+  }
+}
+
+Solver::LsResult Solver::line_search(const Mat& direction, size_t tries) {  // core.rs:99-150
+  const size_t n = nc_;
+  const bool ortho = cfg_.ortho != 0;
+  double alpha = 1.0;
+  LsResult r{false, W_, S_, current_loss_, Mat()};
+  for (size_t k = 0; k < tries; ++k) {
+    Mat transform;
+    if (ortho) {
+      transform = matrix_exp(scale(direction, alpha));
+    } else {
+      transform = Mat::eye(n);
+      for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += alpha * direction.a[e];
+    }
+    r.w = matmul(transform, W_);
+    evaluate(r.w, &r.stats);
+    bool singular;
+    r.loss = loss_of(r.stats, r.w, signs_, &singular);
+    if (r.loss < current_loss_) {
+      r.success = true;
+      r.step = scale(direction, alpha);
+      return r;
+    }
+    alpha /= 2.0;
+  }
+  r.step = scale(direction, alpha);
+  return r;
+}
+
+bool Solver::step() {
+  if (done_) return true;
+  const size_t n = nc_;
+  const double t_f = (double)T_;
+  const bool ortho = cfg_.ortho != 0;
+  last_evals_ = 0;
+  n_iter_ = iter_;
+  // core.rs:215-218 from the pass statistics of the current Y
+  Mat g(n, n);
+  for (size_t e = 0; e < n * n; ++e) g.a[e] = S_.G()[e] / t_f;
+  std::vector<double> dmean(n);
+  for (size_t i = 0; i < n; ++i) dmean[i] = S_.dpsi()[i] / t_f;
+  bool sign_change = false;
+  if (extended_) {  // core.rs:225-253
+    for (size_t i = 0; i < n; ++i) {
+      const double k = dmean[i] * C_(i, i) - g(i, i);
+      signs_[i] = std::isnan(k) ? k : std::copysign(1.0, k);  // f64::signum
+    }
+    if (iter_ > 0)
+      for (size_t i = 0; i < n; ++i)
+        if (signs_[i] != old_signs_[i]) sign_change = true;
+    old_signs_ = signs_;
+    for (size_t i = 0; i < n; ++i) {
+      for (size_t j = 0; j < n; ++j) g(i, j) *= signs_[i];
+      dmean[i] *= signs_[i];  // mean(s_i ψ′_i) = s_i mean(ψ′_i): sign flips are exact
+    }
+    if (!ortho) g = add(g, C_);
+  }
+  std::vector<double> h_off(n, 1.0);  // core.rs:256-260
+  if (ortho)
+    for (size_t i = 0; i < n; ++i) h_off[i] = g(i, i);
+  Mat h(n, n);
+  if (ortho) {  // core.rs:263-272
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = 0; j < n; ++j) {
+        const double v = 0.5 * (dmean[i] + dmean[j] - h_off[i] - h_off[j]);
+        h(i, j) = std::fmax(v, cfg_.lambda_min);
+      }
+  } else {  // core.rs:274-275: ψ′ (signed, +1 when extended) · (Y∘Y)ᵀ / T
+    const double* hr = S_.H();
+    const double* y2 = S_.y2();
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = 0; j < n; ++j) {
+        const double v = extended_ ? signs_[i] * hr[i * n + j] + y2[j] : hr[i * n + j];
+        h(i, j) = v / t_f;
+      }
+    regularize_hessian(h, h_off, cfg_.lambda_min);
+  }
+  if (ortho) {  // core.rs:280-286
+    g = skew_symmetric(g);
+  } else {
+    for (size_t i = 0; i < n; ++i) g(i, i) -= 1.0;
+  }
+  gradient_norm_ = max_abs(g);  // core.rs:289
+  if (gradient_norm_ < cfg_.tol) {
+    converged_ = true;
+    done_ = true;
+    return true;
+  }
+  if (iter_ > 0 && has_prev_step_) {  // core.rs:296-313
+    has_prev_step_ = false;
+    if (has_g_old_) {
+      Mat y_diff = sub(g, g_old_);
+      const double r = 1.0 / dot_sum(prev_step_, y_diff);
+      if (std::isfinite(r)) {
+        mem_.s_list.push_back(prev_step_);
+        mem_.y_list.push_back(y_diff);
+        mem_.r_list.push_back(r);
+        if (mem_.s_list.size() > cfg_.m) {
+          mem_.s_list.pop_front();
+          mem_.y_list.pop_front();
+          mem_.r_list.pop_front();
+        }
+      }
+    }
+  }
+  g_old_ = g;
+  has_g_old_ = true;
+  if (extended_ && sign_change) {  // core.rs:317-331: no extra pass (per-row sums kept)
+    bool singular;
+    current_loss_ = loss_of(S_, W_, signs_, &singular);
+    mem_.clear();
+  }
+  Mat direction = compute_direction(g, h, h_off, mem_, ortho);  // core.rs:334
+  LsResult res = line_search(direction, cfg_.ls_tries);
+  if (!res.success) {  // core.rs:349-364
+    mem_.clear();
+    res = line_search(scale(g, -1.0), 10);
+  }
+  prev_step_ = std::move(res.step);
+  has_prev_step_ = true;
+  W_ = std::move(res.w);
+  S_ = std::move(res.stats);
+  if (extended_ && has_cov_) C_ = matmul_nt(W_, W_);  // core.rs:375-379 with cov = I
+  current_loss_ = res.loss;
+  if (cfg_.verbose)
+    std::printf("iteration %zu, gradient norm = %s, loss = %s\n", iter_ + 1, rust_e4(gradient_norm_).c_str(),
+                rust_e4(current_loss_).c_str());
+  ++iter_;
+  if (iter_ >= cfg_.max_iter) done_ = true;
+  return done_;
+}
+
+static double* dup(const double* p, size_t n) {
+  double* q = new double[n];
+  std::memcpy(q, p, n * sizeof(double));
+  return q;
+}
+
+void Solver::finish(pc_result* out) {
+  std::memset(out, 0, sizeof *out);
+  Mat w = matmul(W_, w_init_);  // solver.rs:169
+  if (!converged_ && cfg_.verbose)
+    std::fprintf(stderr, "Warning: PICARD did not converge. Final gradient norm: %s, tolerance: %s\n",
+                 rust_e4(gradient_norm_).c_str(), rust_e4(cfg_.tol).c_str());
+  if (has_k_) {
+    out->whitening = dup(K_.data(), K_.a.size());
+    out->whitening_rows = K_.rows;
+    out->whitening_cols = K_.cols;
+  }
+  out->unmixing = dup(w.data(), w.a.size());
+  out->unmixing_rows = out->unmixing_cols = nc_;
+  if (cfg_.want_sources) {
+    const uint64_t nl = ev_->n_local();
+    out->sources = new double[nc_ * nl];
+    out->sources_rows = nc_;
+    out->sources_cols = nl;
+    Mat wt = matmul(W_, P_);
+    ev_->sources(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, out->sources);
+  }
+  if (has_mu_) {
+    out->mean = dup(mu_.data(), mu_.size());
+    out->mean_len = mu_.size();
+  }
+  out->n_iterations = n_iter_ + 1;  // core.rs:396
+  out->converged = converged_;
+  out->gradient_norm = gradient_norm_;
+  if (extended_) {
+    out->signs = dup(signs_.data(), signs_.size());
+    out->signs_len = signs_.size();
+  }
+  out->n_evaluations = total_evals_;
+}
+
+// solver.rs:218-249 on the device: with W orthogonal (it is the output of
+// sym_decorrelation), x1 = Wᵀ·(W·x1), so E[g(Wx1) x1ᵀ] = (Σ g(y) yᵀ / p)·W
+// comes from the same fused pass as the Picard gradient.
+Mat Solver::ica_par(const Mat& w_init) {
+  Mat w;
+  if (!sym_decorrelation(w_init, &w)) throw singular_matrix();
+  const double p = (double)T_;
+  const size_t n = nc_;
+  Mat base = has_k_ ? K_ : Mat::eye(nf_);
+  for (uint64_t it = 0; it < cfg_.fastica_it; ++it) {
+    Mat wt = matmul(w, base);
+    EvalStats s;
+    ev_->eval(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, false, &s);
+    Mat graw(n, n);
+    graw.a.assign(s.G(), s.G() + n * n);
+    Mat c = matmul(graw, w);
+    for (double& v : c.a) v /= p;
+    for (size_t i = 0; i < n; ++i) {
+      const double gm = s.dpsi()[i] / p;
+      for (size_t j = 0; j < n; ++j) c(i, j) -= gm * w(i, j);
+    }
+    if (!sym_decorrelation(c, &w)) throw singular_matrix();
+  }
+  if (cfg_.verbose) std::printf("FastICA pre-iterations complete.\n");
+  return w;
+}
+
+// jade.rs:22-72 with the cumulant matrices from the device fourth-moment
+// pass (jade.rs:78-131) and the Jacobi sweeps on rotated copies VᵀMV kept
+// up to date per Givens rotation (same angles as jade.rs:137-185).
+Mat Solver::jade(size_t max_iter, double tol) {
+  const size_t n = nc_;
+  if (n < 2) return Mat::eye(n);
+  const size_t np = n * (n + 1) / 2;
+  std::vector<double> m4(np * np);
+  Mat base = has_k_ ? K_ : Mat::eye(nf_);
+  ev_->moments4(base.data(), n, has_mu_ ? mu_.data() : nullptr, m4.data());
+  std::vector<size_t> pidx(n * n);
+  {
+    size_t q = 0;
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = i; j < n; ++j) { pidx[i * n + j] = pidx[j * n + i] = q++; }
+  }
+  const double t = (double)T_;
+  std::vector<Mat> R;  // rotated cumulant matrices, in jade.rs's (i ≤ j) order
+  R.reserve(np);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = i; j < n; ++j) {
+      Mat q(n, n);
+      const size_t pij = pidx[i * n + j];
+      for (size_t k = 0; k < n; ++k)
+        for (size_t l = 0; l < n; ++l) {
+          double e = m4[pij * np + pidx[k * n + l]] / t;
+          const double d1 = (i == j && k == l) ? 1.0 : 0.0;
+          const double d2 = (i == k && j == l) ? 1.0 : 0.0;
+          const double d3 = (i == l && j == k) ? 1.0 : 0.0;
+          q(k, l) = e - d1 - d2 - d3;
+        }
+      Mat qs(n, n);
+      for (size_t k = 0; k < n; ++k)
+        for (size_t l = 0; l < n; ++l) qs(k, l) = (q(k, l) + q(l, k)) / 2.0;
+      R.push_back(std::move(qs));
+    }
+  if (cfg_.verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
+  Mat v = Mat::eye(n);
+  for (size_t it = 0; it < max_iter; ++it) {
+    double max_theta = 0.0;
+    for (size_t p = 0; p < n; ++p)
+      for (size_t q = p + 1; q < n; ++q) {
+        double g00 = 0, g01 = 0, g11 = 0;
+        for (const Mat& m : R) {
+          const double h_pq = m(p, q) + m(q, p);
+          const double h_pp_qq = m(p, p) - m(q, q);
+          g00 += h_pq * h_pq;
+          g01 += h_pq * h_pp_qq;
+          g11 += h_pp_qq * h_pp_qq;
+        }
+        const double diff = g11 - g00;
+        const double angle = (std::fabs(g01) < 1e-15 && std::fabs(diff) < 1e-15) ? 0.0 : 0.25 * std::atan2(2.0 * g01, diff);
+        const double c = std::cos(angle), s = std::sin(angle);
+        max_theta = std::fmax(max_theta, std::fabs(angle));
+        for (size_t i = 0; i < n; ++i) {  // jade.rs:188-197
+          const double vp = v(i, p), vq = v(i, q);
+          v(i, p) = c * vp - s * vq;
+          v(i, q) = s * vp + c * vq;
+        }
+        // R ← Gᵀ R G with G the same rotation of columns p, q
+#pragma omp parallel for schedule(static)
+        for (long mi = 0; mi < (long)R.size(); ++mi) {
+          Mat& m = R[mi];
+          for (size_t k = 0; k < n; ++k) {
+            const double mp = m(k, p), mq = m(k, q);
+            m(k, p) = c * mp - s * mq;
+            m(k, q) = s * mp + c * mq;
+          }
+          for (size_t k = 0; k < n; ++k) {
+            const double mp = m(p, k), mq = m(q, k);
+            m(p, k) = c * mp - s * mq;
+            m(q, k) = s * mp + c * mq;
+          }
+        }
+      }
+    if (cfg_.verbose && (it + 1) % 10 == 0)
+      std::printf("JADE iteration %zu: max angle = %s\n", it + 1, rust_e4(max_theta).c_str());
+    if (max_theta < tol) {
+      if (cfg_.verbose) std::printf("JADE converged after %zu iterations\n", it + 1);
+      break;
+    }
+  }
+  Mat w;
+  if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
+  return w;
+}
+
+}  // namespace pcamd

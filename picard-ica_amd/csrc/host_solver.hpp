@@ -1,0 +1,77 @@
+// Host Picard driver: src/solver.rs:45-249 + src/core.rs:162-401 +
+// src/lbfgs.rs:84-171 + src/jade.rs:22-197 restated over an Evaluator.
+#pragma once
+#include <deque>
+#include <random>
+
+#include "evaluator.hpp"
+#include "host_linalg.hpp"
+
+namespace pcamd {
+
+std::string rust_e4(double v);  // Rust {:.4e}
+
+// src/lbfgs.rs:6-71 (only the parts core::run uses)
+struct LbfgsMemory {
+  std::deque<Mat> s_list, y_list;
+  std::deque<double> r_list;
+  void clear() { s_list.clear(); y_list.clear(); r_list.clear(); }
+  size_t len() const { return s_list.size(); }
+};
+Mat compute_direction(const Mat& g, const Mat& h, const std::vector<double>& h_off,
+                      const LbfgsMemory& mem, bool ortho);          // lbfgs.rs:84-133
+Mat solve_hessian_system(const Mat& h, const std::vector<double>& h_off, const Mat& g);  // 136-150
+void regularize_hessian(Mat& h, const std::vector<double>& h_off, double lambda_min);   // 155-171
+
+class Solver {
+ public:
+  Solver(Evaluator* ev, const pc_config& cfg);
+  // one iteration of core.rs:211-391; returns true once finished
+  bool step();
+  void finish(pc_result* out);
+  bool done() const { return done_; }
+  double last_loss() const { return current_loss_; }
+  double last_gnorm() const { return gradient_norm_; }
+  uint64_t last_evals() const { return last_evals_; }
+  uint64_t total_evals() const { return total_evals_; }
+
+ private:
+  double loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular);
+  void evaluate(const Mat& w_core, EvalStats* out);
+  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; };
+  LsResult line_search(const Mat& direction, size_t tries);
+  void init_core();
+  Mat ica_par(const Mat& w_init);
+  Mat jade(size_t max_iter, double tol);
+
+  Evaluator* ev_;
+  pc_config cfg_;
+  std::vector<double> w_init_user_;
+  uint64_t nf_ = 0, T_ = 0;
+  size_t nc_ = 0;
+  bool extended_ = false;
+  bool has_mu_ = false;
+  std::vector<double> mu_;
+  bool has_k_ = false;
+  Mat K_;        // whitening (nc × nf)
+  Mat w_init_;   // nc × nc
+  Mat P_;        // w_init·K (nc × nf): maps X−μ to x1 (solver.rs:140)
+  Mat gram_;     // Σ (x−μ)(x−μ)ᵀ when computed
+  bool has_gram_ = false;
+  // core::run state (core.rs:175-209)
+  Mat W_;
+  EvalStats S_;
+  double current_loss_ = 0.0;
+  std::vector<double> signs_, old_signs_;
+  Mat C_;
+  bool has_cov_ = false;
+  LbfgsMemory mem_;
+  bool has_g_old_ = false, has_prev_step_ = false;
+  Mat g_old_, prev_step_;
+  size_t iter_ = 0, n_iter_ = 0;
+  double gradient_norm_ = 1.0;
+  bool converged_ = false, done_ = false;
+  uint64_t last_evals_ = 0, total_evals_ = 0;
+};
+
+}  // namespace pcamd
