@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark: samples/sec per Picard-O iteration at N=128, T=1e8 (+ iterations to tol=1e-7).
+
+Workload (BASELINE.json configs[2] — the config the metric is quoted on; at
+102.4 GB it fits one MI355X's 288 GB, so N=1 runs it whole): 128 sources ×
+1e8 samples of the reference bench mixture (benches/benchmarks.rs:8-35, seed
+42), generated directly in HBM, Picard-O (ortho=True, extended defaults to
+ortho), tanh, tol=1e-7, max_iter=500, m=7, ls_tries=10, whitening + centering.
+
+A "step" is ONE Picard-O iteration (src/core.rs:211-391): every fused pass
+of its line search, the RCCL all-reduce (N>1), the D2H copy and the host N×N
+work. value = T_total × K / (max over ranks of the wall time of K steps), with
+X already resident in HBM. T is sharded in contiguous blocks over ranks
+(strong scaling: the total work is fixed), one RCCL all-reduce of the packed
+statistics per pass.
+
+After the timed region the solver keeps iterating (untimed) to report
+iterations to tol. rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (spec; MI355X_MICROARCH.md); measured 78.0
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--n", type=int, default=128)
+    p.add_argument("--t", type=float, default=1e8)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--to-tol", type=int, default=1, help="continue (untimed) to convergence for iters-to-tol")
+    p.add_argument("--cpu-baseline", type=int, default=1)
+    p.add_argument("--cpu-t", type=float, default=2e5, help="T of the bounded CPU-oracle sample")
+    p.add_argument("--cpu-budget-s", type=float, default=20.0)
+    return p.parse_args()
+
+
+def cpu_baseline(n: int, t: int, seed: int, budget_s: float):
+    """The numpy oracle (oracle/picard_oracle.py, the reference's structure: OpenBLAS
+    dgemm + single-threaded elementwise) timed on this host on a bounded sample."""
+    from oracle import datagen, picard_oracle as po
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
+                    or [os.cpu_count() or 1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    x, _, _ = datagen.generate_data(n, t, seed)
+    xc, _ = po.center(x)
+    x1, _ = po.whiten(xc, n)
+    del x, xc
+    dens = po.Density("tanh", 1.0)
+    # core.rs:162-401: one probe iteration, then as many as fit the budget
+    def timed(k):
+        t0 = time.perf_counter()
+        _, _, info = po.run(x1, dens, True, True, 7, k, 1e-7, 0.01, 10, False, np.eye(n))
+        return info.n_iterations, time.perf_counter() - t0
+    probe = timed(1)
+    k = int(min(64, max(1, budget_s / max(probe[1], 1e-3))))
+    last = timed(k) if k > 1 else probe
+    # samples/s per iteration from the largest run (includes its setup loss pass)
+    return {"value": t * last[0] / last[1], "unit": "samples/s per iteration", "cores": int(cores),
+            "kind": "port",
+            "sample": f"numpy oracle core::run, Picard-O extended tanh, N={n}, T={t} (bench LCG seed {seed}), "
+                      f"{last[0]} iterations in {last[1]:.2f}s; OpenBLAS dgemm threads={cores}, elementwise 1 thread"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n, T = args.n, int(args.t)
+
+    import picard_ica_amd as pa
+
+    dist = None
+    rccl_id = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        dist = dist_mod
+        dist.init_process_group(backend="gloo")
+        obj = [pa.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        rccl_id = obj[0]
+
+    def barrier():
+        pa.device_synchronize(local_rank)
+        if dist is not None:
+            dist.barrier()
+
+    ctx = pa.DeviceContext(local_rank, rank, world, rccl_id)
+    t_gen = time.perf_counter()
+    a_mix = ctx.generate(n, T, args.seed)
+    pa.device_synchronize(local_rank)
+    t_gen = time.perf_counter() - t_gen
+
+    cfg = pa.PicardConfig(ortho=True, max_iter=500, tol=1e-7, random_state=0, want_sources=False)
+    t_setup = time.perf_counter()
+    solver = pa.Solver(ctx, cfg)   # centering, whitening Gram, w_init, initial pass
+    t_setup = time.perf_counter() - t_setup
+
+    done = False
+    for _ in range(args.warmup):
+        if not done:
+            done = solver.step()
+    barrier()
+    ctx.kernel_stats(reset=True)
+    passes = 0
+    t0 = time.perf_counter()
+    steps_run = 0
+    for _ in range(args.steps):
+        if done:
+            break
+        done = solver.step()
+        passes += solver.last()[2]
+        steps_run += 1
+    barrier()
+    elapsed = time.perf_counter() - t0
+    k_ms, call_ms, launches = ctx.kernel_stats(reset=False)
+
+    if dist is not None:
+        import torch
+        t_max = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        elapsed = float(t_max.item())
+
+    iters_to_tol, converged, total_passes = None, None, None
+    t_tol = None
+    if args.to_tol:
+        t1 = time.perf_counter()
+        while not done:
+            done = solver.step()
+        t_tol = time.perf_counter() - t1
+        res = solver.finish()
+        iters_to_tol, converged, total_passes = res.n_iterations, res.converged, res.n_evaluations
+
+    if rank != 0:
+        return
+    steps = max(steps_run, 1)
+    ms_per_step = elapsed / steps * 1e3
+    value = T * steps / elapsed
+    t_local = ctx.n_local
+    avg_k = k_ms / max(launches, 1)
+    flops = 4.0 * n * n * t_local          # ortho fused pass: Y = W·X (2N²T) + ψ·Yᵀ (2N²T)
+    bytes_alg = 8.0 * n * t_local          # one read of the resident X shard
+    achieved_tf = flops / (avg_k * 1e-3) / 1e12 if launches else None
+    roof = {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved_tf / FP64_MFMA_PEAK_TFLOPS if achieved_tf else None, "traffic": None,
+            "kernel": "k_eval_fused<8,false,tanh>", "avg_kernel_ms": avg_k, "launches": launches,
+            "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_alg,
+            "hbm_gbs_algorithmic": bytes_alg / (avg_k * 1e-3) / 1e9 if launches else None}
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                p = json.load(f)
+            if p.get("n") == n and p.get("t_local") == t_local:
+                roof["traffic"] = p.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+    out = {
+        "metric": "samples/sec per Picard-O iter at N=128, T=1e8; iters to tol=1e-7",
+        "value": value, "unit": "samples/s per iteration", "n_gpus": world, "steps": steps_run,
+        "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (benches/benchmarks.rs LCG mixture, seed 42, in HBM)",
+        "config": {"workload": f"Picard-O extended tanh, N={n} sources, T={T} samples (BASELINE configs[2])",
+                   "n_sources": n, "n_samples": T, "ortho": True, "extended": True, "density": "tanh(1)",
+                   "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass"},
+        "passes_per_iter": passes / steps, "iters_to_tol": iters_to_tol, "converged": converged,
+        "total_passes_to_tol": total_passes,
+        "ms_in_kernel_per_step": k_ms / steps, "ms_in_eval_calls_per_step": call_ms / steps,
+        "roofline": roof,
+        "timings_s": {"generate": t_gen, "setup": t_setup, "to_tol_untimed": t_tol},
+    }
+    if args.cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(n, int(args.cpu_t), args.seed, args.cpu_budget_s)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -14,7 +14,7 @@
  *   pc_config_default         ← impl Default for PicardConfig          (src/config.rs:64-85)
  *   pc_config_validate        ← PicardConfig::validate                 (src/config.rs:104-142)
  *   pc_result_free            ← Drop for PicardResult                  (src/result.rs:7)
- *   pc_error_message          ← impl Display for PicardError           (src/error.rs:44-74)
+ *   pc_error_name             ← PicardError variant names              (src/error.rs:9-42)
  *
  * The operator boundary inside core::run (src/core.rs:162-174), i.e. what
  * the HIP kernels replace (score_and_der core.rs:215, the .dot GEMMs
@@ -194,6 +194,13 @@ int pc_fit_with_evaluator(const pc_host_evaluator* ev, const pc_config* cfg, pc_
 /* Timing of the most recent pc_ctx_eval on the context's stream, measured
  * with HIP events around the fused-pass kernel and the whole call. */
 void pc_ctx_last_timing(const pc_ctx* ctx, double* kernel_ms, double* call_ms);
+/* Accumulated over every fused pass since the last reset: total kernel time,
+ * total pc_ctx_eval wall time (upload + kernel + reduce + all-reduce + D2H)
+ * and the number of fused-kernel launches. */
+void pc_ctx_kernel_stats(pc_ctx* ctx, double* kernel_ms, double* call_ms, uint64_t* n_launches,
+                         int32_t reset);
+/* hipDeviceSynchronize on `device` (bench bracketing). */
+int pc_device_synchronize(int32_t device);
 
 #ifdef __cplusplus
 }

@@ -163,6 +163,8 @@ def _load():
         "pc_ctx_sources": (C.c_int, [vp, d, u64, d, d, cp, sz]),
         "pc_ctx_moments4": (C.c_int, [vp, d, u64, d, d, cp, sz]),
         "pc_ctx_last_timing": (None, [vp, d, d]),
+        "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
+        "pc_device_synchronize": (C.c_int, [i32]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -186,7 +188,7 @@ EXPORTED = [
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
-    "pc_ctx_last_timing", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 
@@ -450,6 +452,12 @@ class utils:
 # ------------------------------------------------------------------ device level
 
 
+def device_synchronize(device: int = 0) -> None:
+    rc = lib.pc_device_synchronize(device)
+    if rc:
+        raise ComputationError("hipDeviceSynchronize failed")
+
+
 def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     if lib.pc_rccl_unique_id(buf) != 0:
@@ -526,6 +534,12 @@ class DeviceContext:
         k, c = C.c_double(), C.c_double()
         lib.pc_ctx_last_timing(self.h, C.byref(k), C.byref(c))
         return k.value, c.value
+
+    def kernel_stats(self, reset: bool = False):
+        """(Σ fused-kernel ms, Σ eval-call ms, launches) since the last reset (HIP events)."""
+        k, c, n = C.c_double(), C.c_double(), C.c_uint64()
+        lib.pc_ctx_kernel_stats(self.h, C.byref(k), C.byref(c), C.byref(n), int(reset))
+        return k.value, c.value, n.value
 
     def rowsum(self) -> np.ndarray:
         out = np.empty(self.n_features)

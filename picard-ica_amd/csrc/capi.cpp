@@ -22,6 +22,8 @@ void device_ctx_timing(const Evaluator* e, double* k, double* c);
 void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double* mu, int dens, double alpha,
                          bool need_h, double* stats);
 int rccl_unique_id(char* out);
+void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, uint64_t* n, int reset);
+void device_synchronize(int device);
 }  // namespace pcamd
 
 using namespace pcamd;
@@ -325,6 +327,19 @@ int pc_ctx_moments4(pc_ctx* c, const double* w, uint64_t nc, const double* mu, d
 }
 
 void pc_ctx_last_timing(const pc_ctx* c, double* k, double* call) { device_ctx_timing(c->ev.get(), k, call); }
+
+void pc_ctx_kernel_stats(pc_ctx* c, double* kernel_ms, double* call_ms, uint64_t* n, int32_t reset) {
+  device_ctx_kernel_stats(c->ev.get(), kernel_ms, call_ms, n, reset);
+}
+
+int pc_device_synchronize(int32_t device) {
+  try {
+    device_synchronize(device);
+    return PC_OK;
+  } catch (const PicardError& e) {
+    return e.code;
+  }
+}
 
 int pc_solver_create(pc_ctx* c, const pc_config* cfg, pc_solver** out, char* err, size_t errlen) {
   *out = nullptr;

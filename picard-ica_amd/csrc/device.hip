@@ -534,6 +534,8 @@ struct DeviceCtx : Evaluator {
   double* d_chunk = nullptr; size_t cap_chunk = 0;
   hipEvent_t ev[4];
   double last_kernel_ms = 0, last_call_ms = 0;
+  double sum_kernel_ms = 0, sum_call_ms = 0;
+  uint64_t n_kernel = 0;
 
   DeviceCtx(int dev, int rk, int ws, const char* uid) : device(dev), rank(rk), world(ws) {
     HIP_OK(hipSetDevice(device));
@@ -748,6 +750,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventElapsedTime(&b, ev[0], ev[3]));
     last_kernel_ms = fused ? a : b;
     last_call_ms = b;
+    if (fused) { sum_kernel_ms += a; ++n_kernel; }
+    sum_call_ms += b;
   }
 
   void generic_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st) {
@@ -865,6 +869,17 @@ void device_ctx_timing(const Evaluator* e, double* k, double* c) {
   auto* d = static_cast<const DeviceCtx*>(e);
   *k = d->last_kernel_ms;
   *c = d->last_call_ms;
+}
+void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, uint64_t* n, int reset) {
+  auto* d = static_cast<DeviceCtx*>(e);
+  *kernel_ms = d->sum_kernel_ms;
+  *call_ms = d->sum_call_ms;
+  *n = d->n_kernel;
+  if (reset) { d->sum_kernel_ms = 0; d->sum_call_ms = 0; d->n_kernel = 0; }
+}
+void device_synchronize(int device) {
+  HIP_OK(hipSetDevice(device));
+  HIP_OK(hipDeviceSynchronize());
 }
 void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double* mu, int dens, double alpha,
                          bool need_h, double* stats) {
