@@ -45,28 +45,113 @@ enum { DENS_TANH = 0, DENS_EXP = 1, DENS_CUBE = 2, DENS_LINEAR = 3, DENS_NONE = 
   } while (0)
 
 // ---------------------------------------------------------------------------
+// fp64 elementary functions for the fused pass. fp64 VALU issue and fp64 MFMA
+// share one pipe on gfx950 (tools/microbench/fp64_rates.hip: 78 TF MFMA alone,
+// 66 TF VALU alone, ~75 TF combined), so every VALU op here is paid for in
+// MFMA time. Branch-free, argument ranges known, Chebyshev (near-minimax)
+// coefficients generated with mpmath (tools/gen_coeffs.py): ≤ 2 ulp.
+// ---------------------------------------------------------------------------
+namespace fm {
+constexpr double LOG2E = 0x1.71547652b82fep+0;
+constexpr double LN2_HI = 0x1.62e42fee00000p-1;  // 32 trailing zero bits: k·LN2_HI exact
+constexpr double LN2_LO = 0x1.a39ef35793c76p-33;
+constexpr double LN2 = 0x1.62e42fefa39efp-1;
+constexpr double SQRT2 = 0x1.6a09e667f3bcdp+0;
+
+// x ∈ [-708, 0.35]: e^x = scale·(1 + em_r), scale = 2^k, em_r = e^r − 1, |r| ≤ ln2/2
+__device__ __forceinline__ void exp_parts(double x, double& em_r, double& scale) {
+  const double kf = __builtin_rint(x * LOG2E);
+  double r = __builtin_fma(-kf, LN2_HI, x);
+  r = __builtin_fma(-kf, LN2_LO, r);
+  double p = 0x1.af389ecfc4b9cp-26;
+  p = __builtin_fma(p, r, 0x1.28917c89a43a7p-22);
+  p = __builtin_fma(p, r, 0x1.71de0db2f6b19p-19);
+  p = __builtin_fma(p, r, 0x1.a019b9149a41cp-16);
+  p = __builtin_fma(p, r, 0x1.a01a01a7c2efep-13);
+  p = __builtin_fma(p, r, 0x1.6c16c17889ef1p-10);
+  p = __builtin_fma(p, r, 0x1.11111111109b5p-7);
+  p = __builtin_fma(p, r, 0x1.5555555553d68p-5);
+  p = __builtin_fma(p, r, 0x1.5555555555556p-3);
+  p = __builtin_fma(p, r, 0x1.0000000000001p-1);
+  em_r = __builtin_fma(r * r, p, r);
+  scale = __builtin_ldexp(1.0, (int)kf);
+}
+
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// n / d with one residual correction (≤ 1 ulp)
+__device__ __forceinline__ double div_nr(double n, double d) {
+  const double r = rcp_nr(d);
+  const double q = n * r;
+  return __builtin_fma(__builtin_fma(-d, q, n), r, q);
+}
+
+// ln z for z ∈ [1, 2]: 2·atanh(s), s = (z'−1)/(z'+1), z' = z or z/2 (+ ln 2)
+__device__ __forceinline__ double log_1_2(double z) {
+  const bool big = z > SQRT2;
+  const double zz = big ? 0.5 * z : z;
+  const double s = div_nr(zz - 1.0, zz + 1.0);
+  const double u = s * s;
+  double q = 0x1.2f4d88c4fad06p-4;
+  q = __builtin_fma(q, u, 0x1.3999bf614de60p-4);
+  q = __builtin_fma(q, u, 0x1.7466994f20a7cp-4);
+  q = __builtin_fma(q, u, 0x1.c71c50004ffddp-4);
+  q = __builtin_fma(q, u, 0x1.2492494513f76p-3);
+  q = __builtin_fma(q, u, 0x1.999999997aeaap-3);
+  q = __builtin_fma(q, u, 0x1.55555555555aep-2);
+  q = __builtin_fma(q, u, 0x1.0000000000000p+0);
+  return __builtin_fma(s + s, q, big ? LN2 : 0.0);
+}
+}  // namespace fm
+
+// ---------------------------------------------------------------------------
 // density.rs:50-130 per element. psi = ψ(y), dpsi = ψ′(y), ll = ℓ(y).
 // Tanh: one expm1 feeds both tanh(αy) = −em/(2+em)·sign and
-// ℓ = |y| + ln(1 + e^{−2α|y|})/α = |y| + ln(2 + em)/α.
+// ℓ = |y| + ln(1 + e^{−2α|y|})/α = |y| + ln(2 + em)/α  (α > 0).
+// inv_alpha = 1/α is precomputed (the reference divides; ≤ 1 ulp apart).
 // ---------------------------------------------------------------------------
-template <int DENS>
-__device__ __forceinline__ void density_eval(double y, double alpha, double& psi, double& dpsi, double& ll) {
+template <int DENS, bool FAST>
+__device__ __forceinline__ void density_eval(double y, double alpha, double inv_alpha, double& psi, double& dpsi,
+                                             double& ll) {
   if constexpr (DENS == DENS_TANH) {
-    // em = e^{-2|αy|} − 1; for α > 0 this is also e^{-2α|y|} − 1 (ℓ's term);
-    // for α < 0, e^{-2α|y|} = 1/(1 + em).
     const double ay = fabs(y);
     const double a = alpha * y;
-    const double em = expm1(-2.0 * fabs(a));
-    const double th = copysign(-em / (2.0 + em), a);
-    psi = th;
-    dpsi = alpha * (1.0 - th * th);
-    ll = ay + log(alpha > 0.0 ? 2.0 + em : (2.0 + em) / (1.0 + em)) / alpha;
+    if constexpr (FAST) {  // α > 0 (checked on the host)
+      double em_r, sc;
+      fm::exp_parts(fmax(-2.0 * fabs(a), -708.0), em_r, sc);
+      const double em = __builtin_fma(sc, em_r, sc - 1.0);  // e^{-2|a|} − 1 ∈ (−1, 0]
+      const double z = 2.0 + em;                            // 1 + e^{-2α|y|} ∈ (1, 2]
+      const double th = copysign(fm::div_nr(-em, z), a);
+      psi = th;
+      dpsi = alpha * (1.0 - th * th);
+      ll = ay + fm::log_1_2(z) * inv_alpha;
+    } else {
+      const double th = tanh(a);
+      psi = th;
+      dpsi = alpha * (1.0 - th * th);
+      ll = ay + log(1.0 + exp(-2.0 * alpha * ay)) / alpha;
+    }
   } else if constexpr (DENS == DENS_EXP) {
     const double y2 = y * y;
-    const double k = exp(-alpha / 2.0 * y2);
+    const double x = -alpha / 2.0 * y2;
+    double k;
+    if constexpr (FAST) {  // α > 0: x ≤ 0
+      double em_r, sc;
+      fm::exp_parts(fmax(x, -708.0), em_r, sc);
+      k = __builtin_fma(sc, em_r, sc);
+      ll = -k * inv_alpha;
+    } else {
+      k = exp(x);
+      ll = -exp(-alpha * y * y / 2.0) / alpha;
+    }
     psi = y * k;
     dpsi = (1.0 - alpha * y2) * k;
-    ll = -k / alpha;
   } else if constexpr (DENS == DENS_CUBE) {
     const double y2 = y * y;
     psi = y2 * y;
@@ -107,6 +192,10 @@ __host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
   return (size_t)(need_h ? 2 : 1) * ncp * ncp + 3 * (size_t)ncp;
 }
 
+// Software-pipelined over blocks with ONE barrier per block: iteration b
+// runs the Y stage of block b+1 (one dependent MFMA chain) next to the G
+// stage of block b (GI·GJ independent accumulators), so the chain's latency
+// hides under independent MFMAs; X tiles and ψ/Y images are double-buffered.
 template <int NB, bool NEED_H, int DENS>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int nfp,
@@ -117,12 +206,13 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int yi = wave % NB, yts = wave / NB;
+  const double inv_alpha = 1.0 / alpha;
 
   extern __shared__ double smem[];
-  double* xs = smem;                         // [TS][nfp][16]
-  double* psis = xs + TS * nfp * 16;         // [KK][NB][64]
-  double* ys = psis + S::FRAGS;              // [KK][NB][64]
-  double* dps = ys + S::FRAGS;               // [KK][NB][64] (NEED_H)
+  const int xs_sz = TS * nfp * 16;
+  double* xs0 = smem;                            // [2][TS][nfp][16]
+  double* img0 = smem + 2 * xs_sz;               // [2][NIMG][KK][NB][64]
+  constexpr int NIMG = NEED_H ? 3 : 2;           // ψ, y (, ψ′)
 
   const int ks_n = nfp >> 2;
   double wf[KSMAX];
@@ -160,7 +250,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       }
     }
   };
-  auto store_x = [&](uint64_t b) {
+  auto store_x = [&](uint64_t b, double* xs) {
 #pragma unroll
     for (int p = 0; p < PRE; ++p) {
       const int e = tid + p * FUSED_THREADS;
@@ -175,44 +265,40 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       }
     }
   };
-
-  if (b_begin < b_end) load_x(b_begin);
-  for (uint64_t b = b_begin; b < b_end; ++b) {
-    store_x(b);
-    __syncthreads();  // (A) X tile visible; previous G stage finished everywhere
-    if (b + 1 < b_end) load_x(b + 1);
-
-    // ---- Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over nf
+  // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over nf
+  auto y_stage = [&](const double* xs) {
     d4 yv = d4{0, 0, 0, 0};
     const double* xrow = xs + (yts * nfp + lk) * 16 + lr;
 #pragma unroll
     for (int ks = 0; ks < KSMAX; ++ks)
       if (ks < ks_n) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
-
-    // ---- elementwise density, row sums, hand-off through LDS
+    return yv;
+  };
+  // density on the tile, row sums, hand-off of the ψ / y (/ ψ′) fragments
+  auto elementwise = [&](const d4& yv, uint64_t b, double* img) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const double y = yv[r];
       double psi, dpsi, ll;
-      density_eval<DENS>(y, alpha, psi, dpsi, ll);
+      density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
       const uint64_t tg = b * TB + yts * 16 + 4 * r + lk;
       if (tg < n_local) { rs_dpsi += dpsi; rs_ll += ll; rs_y2 += y * y; }
-      const int kk = yts * 4 + r;
-      psis[(kk * NB + yi) * 64 + lane] = psi;
-      ys[(kk * NB + yi) * 64 + lane] = y;
-      if constexpr (NEED_H) dps[(kk * NB + yi) * 64 + lane] = dpsi;
+      const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
+      img[f] = psi;
+      img[S::FRAGS + f] = y;
+      if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi;
     }
-    __syncthreads();  // (B) ψ / y images complete; X tile no longer read
-
-    // ---- G stage: G_raw[i-blocks][j-blocks] += ψ · Yᵀ over this block's samples
+  };
+  // G stage: G_raw[i-blocks][j-blocks] += ψ · Yᵀ (H_raw += ψ′ · (Y∘Y)ᵀ) over one block
+  auto g_stage = [&](const double* img) {
 #pragma unroll
     for (int q = 0; q < KKW; ++q) {
       const int kk = kk0 + q;
       double pa[GI], yf[GJ];
 #pragma unroll
-      for (int i = 0; i < GI; ++i) pa[i] = psis[(kk * NB + gi0 + i) * 64 + lane];
+      for (int i = 0; i < GI; ++i) pa[i] = img[(kk * NB + gi0 + i) * 64 + lane];
 #pragma unroll
-      for (int j = 0; j < GJ; ++j) yf[j] = ys[(kk * NB + gj0 + j) * 64 + lane];
+      for (int j = 0; j < GJ; ++j) yf[j] = img[S::FRAGS + (kk * NB + gj0 + j) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < GI; ++i)
 #pragma unroll
@@ -220,17 +306,47 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       if constexpr (NEED_H) {
 #pragma unroll
         for (int i = 0; i < GI; ++i) {
-          const double da = dps[(kk * NB + gi0 + i) * 64 + lane];
+          const double da = img[2 * S::FRAGS + (kk * NB + gi0 + i) * 64 + lane];
 #pragma unroll
           for (int j = 0; j < GJ; ++j) acch[i][j] = mfma(da, yf[j] * yf[j], acch[i][j]);
         }
       }
     }
+  };
+
+  if (b_begin < b_end) {
+    // prologue: X(b0) → xs[0]; Y + density of b0 → img[0]; X(b0+1) → xs[1]
+    load_x(b_begin);
+    store_x(b_begin, xs0);
+    if (b_begin + 1 < b_end) load_x(b_begin + 1);
+    __syncthreads();
+    elementwise(y_stage(xs0), b_begin, img0);
+    if (b_begin + 1 < b_end) {
+      store_x(b_begin + 1, xs0 + xs_sz);
+      if (b_begin + 2 < b_end) load_x(b_begin + 2);
+    }
+    __syncthreads();
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      const int cur = (int)((b - b_begin) & 1);
+      double* xs_next = xs0 + (cur ^ 1) * xs_sz;
+      double* img_cur = img0 + cur * NIMG * S::FRAGS;
+      double* img_next = img0 + (cur ^ 1) * NIMG * S::FRAGS;
+      const bool has_next = b + 1 < b_end;
+      d4 yv = d4{0, 0, 0, 0};
+      if (has_next) yv = y_stage(xs_next);
+      g_stage(img_cur);
+      if (has_next) elementwise(yv, b + 1, img_next);
+      if (b + 2 < b_end) {
+        store_x(b + 2, xs0 + cur * xs_sz);
+        if (b + 3 < b_end) load_x(b + 3);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: per-workgroup partials [G | H | Σψ′ | Σℓ | Σy²]
   double* out = partials + (size_t)blockIdx.x * fused_partial_stride(NCP, NEED_H);
-  __syncthreads();
+  double* red = img0;  // scratch (all waves are past the last barrier)
   if constexpr (S::KSPL == 1) {
 #pragma unroll
     for (int i = 0; i < GI; ++i)
@@ -244,7 +360,6 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
         }
   } else {
     // waves that split one G block's k range meet in LDS, summed in wave order
-    double* red = psis;  // KSPL × blocks × 256 (+ the same for H)
     constexpr int NBLK = NB * NB;
     const int blk = gi0 * NB + gj0;
     const int sp = kk0 / KKW;
@@ -273,7 +388,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   rs_dpsi += __shfl_xor(rs_dpsi, 16); rs_dpsi += __shfl_xor(rs_dpsi, 32);
   rs_ll += __shfl_xor(rs_ll, 16);     rs_ll += __shfl_xor(rs_ll, 32);
   rs_y2 += __shfl_xor(rs_y2, 16);     rs_y2 += __shfl_xor(rs_y2, 32);
-  double* rsb = ys;  // [TS][NCP][3]
+  double* rsb = xs0;  // [TS][NCP][3]
   if (lk == 0) {
     rsb[(yts * NCP + yi * 16 + lr) * 3 + 0] = rs_dpsi;
     rsb[(yts * NCP + yi * 16 + lr) * 3 + 1] = rs_ll;
@@ -283,9 +398,9 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   double* orow = out + (size_t)(NEED_H ? 2 : 1) * NCP * NCP;
   for (int e = tid; e < NCP * 3; e += FUSED_THREADS) {
     const int row = e / 3, c = e % 3;
-    double s = 0.0;
-    for (int ts = 0; ts < TS; ++ts) s += rsb[(ts * NCP + row) * 3 + c];
-    orow[c * NCP + row] = s;
+    double sum = 0.0;
+    for (int ts = 0; ts < TS; ++ts) sum += rsb[(ts * NCP + row) * 3 + c];
+    orow[c * NCP + row] = sum;
   }
 }
 
@@ -342,7 +457,7 @@ __global__ void k_ycomp(const double* __restrict__ X, uint64_t ldx, uint64_t n_v
       if (Y) Y[(size_t)(i0 + r) * ldy + t] = y;
       if constexpr (DENS != DENS_NONE) {
         double psi, dpsi, ll;
-        density_eval<DENS>(y, alpha, psi, dpsi, ll);
+        density_eval<DENS, false>(y, alpha, 1.0 / alpha, psi, dpsi, ll);
         P[(size_t)(i0 + r) * ldc + t] = psi;
         D[(size_t)(i0 + r) * ldc + t] = valid ? dpsi : 0.0;
         L[(size_t)(i0 + r) * ldc + t] = valid ? ll : 0.0;
@@ -681,7 +796,7 @@ struct DeviceCtx : Evaluator {
     nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
     const size_t pstride = fused_partial_stride(S::NCP, H);
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
-    const size_t lds = (size_t)(S::TS * nfp * 16 + (H ? 3 : 2) * S::FRAGS) * sizeof(double);
+    const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
     auto kern = k_eval_fused<NB, H, D>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -719,7 +834,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventRecord(ev[0], stream));
     const int nb = pick_nb(nc);
     const int nfp = (int)((nf + 3) / 4 * 4);
-    const bool fused = nb > 0 && nfp <= 4 * KSMAX && (8 / nb) * nfp <= 128 && !(need_h && nb == 8);
+    const bool fused = nb > 0 && nfp <= 4 * KSMAX && (8 / nb) * nfp <= 128 && !(need_h && nb == 8) &&
+                       !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0));
     double* dmu = nullptr;
     if (mu) {
       dmu = ensure(d_mu, cap_mu, std::max<size_t>(nfp, nf));

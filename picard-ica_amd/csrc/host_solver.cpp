@@ -201,7 +201,10 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   // x1 = w_init·x1 (solver.rs:140), kept as the composed map P
   P_ = has_k_ ? matmul(w_init_, K_) : w_init_;
   has_cov_ = extended_ && cfg.whiten;  // solver.rs:143-147
-  if (cfg.verbose) std::printf("Running Picard...\n");
+  if (cfg.verbose) {
+    std::printf("Running Picard...\n");
+    std::fflush(stdout);
+  }
   init_core();
 }
 
@@ -388,6 +391,7 @@ bool Solver::step() {
   if (cfg_.verbose)
     std::printf("iteration %zu, gradient norm = %s, loss = %s\n", iter_ + 1, rust_e4(gradient_norm_).c_str(),
                 rust_e4(current_loss_).c_str());
+  if (cfg_.verbose) std::fflush(stdout);
   ++iter_;
   if (iter_ >= cfg_.max_iter) done_ = true;
   return done_;

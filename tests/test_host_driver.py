@@ -1,0 +1,107 @@
+"""The C++ host driver (core::run, L-BFGS, line search, whitening, warm starts)
+run through pc_fit_with_evaluator with the per-pass statistics supplied by
+callbacks. The callbacks compute the same sums the HIP pass produces, so this
+checks the host logic against the oracle on a CPU-only machine. The product
+path never uses these callbacks (they are a test hook of the C ABI)."""
+import numpy as np
+import pytest
+
+from conftest import density_of
+
+
+def host_fit(pa, po, x, cfg):
+    def ev(w, mu, d, need_h):
+        return po.pass_stats(w, mu, x, density_of(po, d), need_h)
+
+    def gram(mu):
+        xc = x - mu[:, None] if mu is not None else x
+        return xc @ xc.T
+
+    def sources(w, mu):
+        return w @ (x - mu[:, None] if mu is not None else x)
+
+    def m4(w, mu):
+        y = sources(w, mu)
+        n = y.shape[0]
+        z = np.stack([y[i] * y[j] for i in range(n) for j in range(i, n)])
+        return z @ z.T
+
+    return pa.fit_with_host_evaluator(x.shape[0], x.shape[1], cfg, rowsum=lambda: x.sum(axis=1), gram=gram,
+                                      eval=ev, sources=sources, moments4=m4)
+
+
+@pytest.mark.parametrize("ortho,extended", [(True, True), (True, False), (False, True), (False, False)])
+def test_core_run_matches_oracle(pa, po, c1_data, ortho, extended):
+    x, s, a = c1_data
+    r = host_fit(pa, po, x, pa.PicardConfig(w_init=np.eye(8), ortho=ortho, extended=extended))
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(8), ortho=ortho, extended=extended))
+    assert r.converged and ro.converged
+    assert abs(r.n_iterations - ro.n_iterations) <= 2
+    if ortho:  # identical trajectories: same pass count, W to rounding
+        assert r.n_iterations == ro.n_iterations and r.n_evaluations == ro.info.n_evals
+        assert np.max(np.abs(r.unmixing - ro.unmixing)) < 1e-10
+    assert abs(pa.utils.amari_distance(r.full_unmixing(), a) - po.amari_distance(ro.full_unmixing(), a)) < 1e-6
+    assert np.max(np.abs(r.whitening - ro.whitening)) < 1e-8
+
+
+@pytest.mark.parametrize("kw", [dict(n_components=5), dict(whiten=False), dict(centering=False),
+                                dict(whiten=False, extended=True, ortho=False), dict(fastica_it=5),
+                                dict(jade_it=2), dict(m=2, ls_tries=3), dict(lambda_min=0.5), dict(tol=1e-4)])
+def test_config_variants(pa, po, c1_data, kw):
+    x, s, a = c1_data
+    nc = kw.get("n_components", 8)
+    r = host_fit(pa, po, x, pa.PicardConfig(w_init=np.eye(nc), max_iter=300, **kw))
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(nc), max_iter=300, **kw))
+    assert r.converged == ro.converged
+    fw, fwo = r.full_unmixing(), ro.full_unmixing()
+    assert np.max(np.abs(fw - fwo)) <= 1e-6 * np.max(np.abs(fwo))
+    assert (r.whitening is None) == (ro.whitening is None)
+    assert (r.mean is None) == (ro.mean is None)
+
+
+@pytest.mark.parametrize("dens", [("exp", 1.0), ("cube", 1.0), ("tanh", 0.5)])
+def test_densities(pa, po, c1_data, dens):
+    x, s, a = c1_data
+    pd = pa.DensityType(["tanh", "exp", "cube"].index(dens[0]), dens[1])
+    r = host_fit(pa, po, x, pa.PicardConfig(w_init=np.eye(8), density=pd, max_iter=200))
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(8), density=po.Density(*dens), max_iter=200))
+    assert r.n_iterations == ro.n_iterations and r.converged == ro.converged
+    assert np.max(np.abs(r.unmixing - ro.unmixing)) < 1e-8
+
+
+def test_max_iter_and_counts(pa, po, c1_data):
+    x, s, a = c1_data
+    r = host_fit(pa, po, x, pa.PicardConfig(w_init=np.eye(8), max_iter=3))
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(8), max_iter=3))
+    assert r.n_iterations == ro.n_iterations == 3  # core.rs:396 (last iter + 1)
+    assert not r.converged
+    assert np.max(np.abs(r.unmixing - ro.unmixing)) < 1e-10
+
+
+def test_verbose_lines(pa, po, c1_data, capfd):
+    x, s, a = c1_data
+    host_fit(pa, po, x, pa.PicardConfig(w_init=np.eye(8), max_iter=2, verbose=True))
+    out = capfd.readouterr().out.splitlines()
+    assert out[0] == "Running Picard..."
+    assert out[1].startswith("iteration 1, gradient norm = ") and ", loss = " in out[1]
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(8), max_iter=2))
+    assert out[1] == (f"iteration 1, gradient norm = {po.rust_e4(ro.info.trace_gnorm[0])}, "
+                      f"loss = {po.rust_e4(ro.info.trace_loss[0])}")
+
+
+def test_errors(pa, po, c1_data):
+    x, s, a = c1_data
+    with pytest.raises(pa.InvalidDimensions, match=r"w_init shape \[3, 3\] doesn't match expected \(8, 8\)"):
+        host_fit(pa, po, x, pa.PicardConfig(w_init=np.eye(3)))
+    with pytest.raises(pa.InvalidConfig):
+        host_fit(pa, po, x, pa.PicardConfig(m=0))
+    with pytest.raises(pa.SingularMatrix):
+        host_fit(pa, po, np.ones((3, 50)), pa.PicardConfig())
+
+
+def test_seeded_random_init_is_deterministic(pa, po, c1_data):
+    x, s, a = c1_data
+    r1 = host_fit(pa, po, x, pa.PicardConfig(random_state=7))
+    r2 = host_fit(pa, po, x, pa.PicardConfig(random_state=7))
+    assert np.array_equal(r1.unmixing, r2.unmixing)
+    assert r1.converged and po.amari_distance(r1.full_unmixing(), a) < 0.01
