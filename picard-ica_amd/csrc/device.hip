@@ -193,31 +193,38 @@ __host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
 }
 
 // Software-pipelined over blocks with ONE barrier per block: iteration b
-// runs the Y stage of block b+1 (one dependent MFMA chain) next to the G
-// stage of block b (GI·GJ independent accumulators), so the chain's latency
-// hides under independent MFMAs; X tiles and ψ/Y images are double-buffered.
+// runs the Y stage of block b+1 (two interleaved MFMA chains) next to the G
+// stage of block b (GI·GJ independent accumulators) in one basic block, so
+// the chains' latency hides under independent MFMAs; X tiles and ψ/Y images
+// are double-buffered. Loads/stores of X use clamped block indices and
+// selects instead of branches (the last iteration is peeled).
+// X rows are padded to ldx ≡ 0 (mod 128) so a TB-sample tile never crosses a row end.
 template <int NB, bool NEED_H, int DENS>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
-k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int nfp,
+k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf,
              const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
              uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials) {
   using S = FusedShape<NB>;
   constexpr int TS = S::TS, TB = S::TB, NCP = S::NCP, KKW = S::KKW, GI = S::GI, GJ = S::GJ;
+  constexpr int NFP = 16 * NB;       // K of the Y stage, padded (zero X rows / zero W columns)
+  constexpr int KS = NFP / 4;        // MFMA k-steps of the Y stage
+  constexpr int XS = TS * NFP * 16;  // doubles per X tile (= 2048 for every NB)
+  constexpr int N2 = XS / 2;         // double2 per X tile
+  constexpr int PRE = N2 / FUSED_THREADS;
+  static_assert(N2 % FUSED_THREADS == 0, "X tile must split evenly over the workgroup");
+  constexpr int NIMG = NEED_H ? 3 : 2;  // ψ, y (, ψ′) images
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int yi = wave % NB, yts = wave / NB;
   const double inv_alpha = 1.0 / alpha;
 
   extern __shared__ double smem[];
-  const int xs_sz = TS * nfp * 16;
-  double* xs0 = smem;                            // [2][TS][nfp][16]
-  double* img0 = smem + 2 * xs_sz;               // [2][NIMG][KK][NB][64]
-  constexpr int NIMG = NEED_H ? 3 : 2;           // ψ, y (, ψ′)
+  double* xs0 = smem;             // [2][TS][NFP][16]
+  double* img0 = smem + 2 * XS;   // [2][NIMG][KK][NB][64]
 
-  const int ks_n = nfp >> 2;
-  double wf[KSMAX];
+  double wf[KS];
 #pragma unroll
-  for (int ks = 0; ks < KSMAX; ++ks) wf[ks] = ks < ks_n ? Wp[(yi * 16 + lr) * nfp + 4 * ks + lk] : 0.0;
+  for (int ks = 0; ks < KS; ++ks) wf[ks] = Wp[(yi * 16 + lr) * NFP + 4 * ks + lk];
 
   int gi0, gj0, kk0;
   if constexpr (NB == 8) { gi0 = (wave >> 2) * 4; gj0 = (wave & 3) * 2; kk0 = 0; }
@@ -235,44 +242,48 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
-  const int n2 = nfp * TB / 2;  // double2 elements per X tile
-  constexpr int PRE = 2;        // ≥ n2 / 512 (TS·nfp ≤ 128 is checked on the host)
+  const uint64_t b_last = b_end - 1;
 
+  // per-thread X staging slots: row k, sample pair t (fixed for the launch)
+  int xk[PRE], xt[PRE];
+  double xmu[PRE];
+  bool xrow_ok[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) {
+    const int e = tid + p * FUSED_THREADS;
+    xk[p] = e / (TB / 2);
+    xt[p] = 2 * (e % (TB / 2));
+    xrow_ok[p] = xk[p] < nf;
+    xmu[p] = (xrow_ok[p] && mu) ? mu[xk[p]] : 0.0;
+  }
   double2 pre[PRE];
-  auto load_x = [&](uint64_t b) {
+  auto load_x = [&](uint64_t b) {  // b ≤ b_last: always a valid address
 #pragma unroll
     for (int p = 0; p < PRE; ++p) {
-      const int e = tid + p * FUSED_THREADS;
-      if (e < n2) {
-        const int k = e / (TB / 2), t = 2 * (e % (TB / 2));
-        if (k < nf && b * TB + t < ldx) pre[p] = *reinterpret_cast<const double2*>(X + (size_t)k * ldx + b * TB + t);
-        else pre[p] = double2{0.0, 0.0};
-      }
+      const int k = xrow_ok[p] ? xk[p] : 0;
+      pre[p] = *reinterpret_cast<const double2*>(X + (size_t)k * ldx + b * TB + xt[p]);
     }
   };
   auto store_x = [&](uint64_t b, double* xs) {
 #pragma unroll
     for (int p = 0; p < PRE; ++p) {
-      const int e = tid + p * FUSED_THREADS;
-      if (e < n2) {
-        const int k = e / (TB / 2), t = 2 * (e % (TB / 2));
-        const uint64_t tg = b * TB + t;
-        const double m = (k < nf && mu) ? mu[k] : 0.0;
-        double2 v;
-        v.x = (k < nf && tg < n_local) ? pre[p].x - m : 0.0;
-        v.y = (k < nf && tg + 1 < n_local) ? pre[p].y - m : 0.0;
-        *reinterpret_cast<double2*>(xs + ((t >> 4) * nfp + k) * 16 + (t & 15)) = v;
-      }
+      const uint64_t tg = b * TB + xt[p];
+      double2 v;
+      v.x = (xrow_ok[p] && tg < n_local) ? pre[p].x - xmu[p] : 0.0;
+      v.y = (xrow_ok[p] && tg + 1 < n_local) ? pre[p].y - xmu[p] : 0.0;
+      *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
     }
   };
-  // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over nf
+  // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over NFP, as two chains
   auto y_stage = [&](const double* xs) {
-    d4 yv = d4{0, 0, 0, 0};
-    const double* xrow = xs + (yts * nfp + lk) * 16 + lr;
+    d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0};
+    const double* xrow = xs + (yts * NFP + lk) * 16 + lr;
 #pragma unroll
-    for (int ks = 0; ks < KSMAX; ++ks)
-      if (ks < ks_n) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
-    return yv;
+    for (int ks = 0; ks < KS; ks += 2) {
+      ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+      yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
+    }
+    return ya + yb;
   };
   // density on the tile, row sums, hand-off of the ψ / y (/ ψ′) fragments
   auto elementwise = [&](const d4& yv, uint64_t b, double* img) {
@@ -281,8 +292,10 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       const double y = yv[r];
       double psi, dpsi, ll;
       density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
-      const uint64_t tg = b * TB + yts * 16 + 4 * r + lk;
-      if (tg < n_local) { rs_dpsi += dpsi; rs_ll += ll; rs_y2 += y * y; }
+      const bool valid = b * TB + yts * 16 + 4 * r + lk < n_local;
+      rs_dpsi += valid ? dpsi : 0.0;
+      rs_ll += valid ? ll : 0.0;
+      rs_y2 += y * y;  // y = 0 exactly for samples past the end (zero X columns)
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
       img[f] = psi;
       img[S::FRAGS + f] = y;
@@ -315,33 +328,28 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   };
 
   if (b_begin < b_end) {
+    auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
     // prologue: X(b0) → xs[0]; Y + density of b0 → img[0]; X(b0+1) → xs[1]
     load_x(b_begin);
     store_x(b_begin, xs0);
-    if (b_begin + 1 < b_end) load_x(b_begin + 1);
+    load_x(clampb(b_begin + 1));
     __syncthreads();
     elementwise(y_stage(xs0), b_begin, img0);
-    if (b_begin + 1 < b_end) {
-      store_x(b_begin + 1, xs0 + xs_sz);
-      if (b_begin + 2 < b_end) load_x(b_begin + 2);
-    }
+    store_x(clampb(b_begin + 1), xs0 + XS);
+    load_x(clampb(b_begin + 2));
     __syncthreads();
-    for (uint64_t b = b_begin; b < b_end; ++b) {
-      const int cur = (int)((b - b_begin) & 1);
-      double* xs_next = xs0 + (cur ^ 1) * xs_sz;
-      double* img_cur = img0 + cur * NIMG * S::FRAGS;
-      double* img_next = img0 + (cur ^ 1) * NIMG * S::FRAGS;
-      const bool has_next = b + 1 < b_end;
-      d4 yv = d4{0, 0, 0, 0};
-      if (has_next) yv = y_stage(xs_next);
-      g_stage(img_cur);
-      if (has_next) elementwise(yv, b + 1, img_next);
-      if (b + 2 < b_end) {
-        store_x(b + 2, xs0 + cur * xs_sz);
-        if (b + 3 < b_end) load_x(b + 3);
-      }
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_last; ++b) {
+      const d4 yv = y_stage(xs0 + (cur ^ 1) * XS);     // block b+1
+      g_stage(img0 + cur * NIMG * S::FRAGS);           // block b
+      elementwise(yv, b + 1, img0 + (cur ^ 1) * NIMG * S::FRAGS);
+      store_x(clampb(b + 2), xs0 + cur * XS);
+      load_x(clampb(b + 3));
       __syncthreads();
+      cur ^= 1;
     }
+    g_stage(img0 + cur * NIMG * S::FRAGS);  // block b_last
+    __syncthreads();
   }
 
   // ---- epilogue: per-workgroup partials [G | H | Σψ′ | Σℓ | Σy²]
@@ -692,8 +700,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     if (X) HIP_OK(hipFree(X));
     nf = nf_; n_local_ = n_local; n_total = n_tot; t0 = t0_;
-    ldx = (n_local + 15) / 16 * 16;
-    if (ldx == 0) ldx = 16;
+    ldx = (n_local + 127) / 128 * 128;  // a fused-pass tile (≤ 128 samples) never crosses a row end
+    if (ldx == 0) ldx = 128;
     HIP_OK(hipMalloc(&X, nf * ldx * sizeof(double) + 256));
     HIP_OK(hipMemsetAsync(X, 0, nf * ldx * sizeof(double) + 256, stream));
   }
@@ -797,6 +805,7 @@ struct DeviceCtx : Evaluator {
     const size_t pstride = fused_partial_stride(S::NCP, H);
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
+    (void)nfp;
     auto kern = k_eval_fused<NB, H, D>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -804,7 +813,7 @@ struct DeviceCtx : Evaluator {
       attr_set = true;
     }
     HIP_OK(hipEventRecord(ev[1], stream));
-    kern<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, nfp, d_w, dmu, alpha, bpw, n_blocks, part);
+    kern<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t total = EvalStats::size(nc, H);
@@ -833,8 +842,8 @@ struct DeviceCtx : Evaluator {
     double* st = ensure(d_stats, cap_stats, total);
     HIP_OK(hipEventRecord(ev[0], stream));
     const int nb = pick_nb(nc);
-    const int nfp = (int)((nf + 3) / 4 * 4);
-    const bool fused = nb > 0 && nfp <= 4 * KSMAX && (8 / nb) * nfp <= 128 && !(need_h && nb == 8) &&
+    const int nfp = 16 * std::max(nb, 1);  // fused pass: K padded to 16·NB (host builds Wp accordingly)
+    const bool fused = nb > 0 && nf <= (uint64_t)nfp && !(need_h && nb == 8) &&
                        !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0));
     double* dmu = nullptr;
     if (mu) {
