@@ -121,6 +121,7 @@ def main():
             done = solver.step()
     barrier()
     ctx.kernel_stats(reset=True)
+    ctx.kernel_breakdown(reset=True)
     passes = 0
     t0 = time.perf_counter()
     steps_run = 0
@@ -133,6 +134,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     k_ms, call_ms, launches = ctx.kernel_stats(reset=False)
+    brk = ctx.kernel_breakdown(reset=False)
 
     if dist is not None:
         import torch
@@ -184,7 +186,9 @@ def main():
                    "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass"},
         "passes_per_iter": passes / steps, "iters_to_tol": iters_to_tol, "converged": converged,
         "total_passes_to_tol": total_passes,
-        "ms_in_kernel_per_step": k_ms / steps, "ms_in_eval_calls_per_step": call_ms / steps,
+        "ms_in_eval_calls_per_step": call_ms / steps,
+        "kernels_per_step": {k: {"ms": v[0] / steps, "launches": v[1] / steps,
+                                 "avg_ms": (v[0] / v[1]) if v[1] else None} for k, v in brk.items()},
         "roofline": roof,
         "timings_s": {"generate": t_gen, "setup": t_setup, "to_tol_untimed": t_tol},
     }

@@ -149,6 +149,18 @@ enum { PC_EVAL_NEED_H = 1u };
 int pc_ctx_eval(pc_ctx* ctx, const double* w /* nc × n_features */, uint64_t nc,
                 const double* mu /* n_features or NULL */, pc_density density, uint32_t flags,
                 double* stats, char* err, size_t errlen);
+/* Split form of pc_ctx_eval for line-search tries (core.rs:117-140 only needs
+ * Σℓ and Σy² to accept or reject a try). pc_ctx_eval_loss fills the Σℓ, Σy²
+ * entries of `stats` (same layout as pc_ctx_eval) from a pass that skips the
+ * ψ·Yᵀ contraction and keeps Y in HBM; *kept = 1 then, and
+ * pc_ctx_eval_complete fills the remaining entries (G_raw, H_raw, Σψ′) for the
+ * same W from the kept Y. *kept = 0 means the pass was a full pc_ctx_eval
+ * (shape not covered or HBM too short to keep Y). Sums are bit-identical to
+ * pc_ctx_eval's. */
+int pc_ctx_eval_loss(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, pc_density density,
+                     uint32_t flags, double* stats, int32_t* kept, char* err, size_t errlen);
+int pc_ctx_eval_complete(pc_ctx* ctx, pc_density density, uint32_t flags, double* stats, char* err,
+                         size_t errlen);
 int pc_ctx_rowsum(pc_ctx* ctx, double* out /* n_features */, char* err, size_t errlen);
 int pc_ctx_gram(pc_ctx* ctx, const double* mu /* or NULL */, double* out /* nf × nf */,
                 char* err, size_t errlen);
@@ -199,6 +211,9 @@ void pc_ctx_last_timing(const pc_ctx* ctx, double* kernel_ms, double* call_ms);
  * and the number of fused-kernel launches. */
 void pc_ctx_kernel_stats(pc_ctx* ctx, double* kernel_ms, double* call_ms, uint64_t* n_launches,
                          int32_t reset);
+/* Per kernel kind since the last reset: [0] fused pass, [1] loss-only try,
+ * [2] completion from kept Y — summed HIP-event kernel ms and launch counts. */
+void pc_ctx_kernel_breakdown(pc_ctx* ctx, double ms[3], uint64_t n[3], int32_t reset);
 /* hipDeviceSynchronize on `device` (bench bracketing). */
 int pc_device_synchronize(int32_t device);
 

@@ -158,6 +158,8 @@ def _load():
         "pc_ctx_n_local": (u64, [vp]),
         "pc_ctx_t0": (u64, [vp]),
         "pc_ctx_eval": (C.c_int, [vp, d, u64, d, _Density, C.c_uint32, d, cp, sz]),
+        "pc_ctx_eval_loss": (C.c_int, [vp, d, u64, d, _Density, C.c_uint32, d, P(i32), cp, sz]),
+        "pc_ctx_eval_complete": (C.c_int, [vp, _Density, C.c_uint32, d, cp, sz]),
         "pc_ctx_rowsum": (C.c_int, [vp, d, cp, sz]),
         "pc_ctx_gram": (C.c_int, [vp, d, d, cp, sz]),
         "pc_ctx_sources": (C.c_int, [vp, d, u64, d, d, cp, sz]),
@@ -165,6 +167,7 @@ def _load():
         "pc_ctx_last_timing": (None, [vp, d, d]),
         "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
         "pc_device_synchronize": (C.c_int, [i32]),
+        "pc_ctx_kernel_breakdown": (None, [vp, d, P(u64), i32]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -187,8 +190,8 @@ EXPORTED = [
     "pc_full_unmixing", "pc_mixing", "pc_result_free", "pc_amari_distance", "pc_permute",
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
-    "pc_ctx_eval", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
-    "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
+    "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 
@@ -530,6 +533,32 @@ class DeviceContext:
         out["dpsi"], out["ll"], out["y2"] = st[o:o + nc], st[o + nc:o + 2 * nc], st[o + 2 * nc:o + 3 * nc]
         return out
 
+    @staticmethod
+    def _unpack(st, nc, need_h):
+        o = nc * nc
+        out = {"G": st[:o].reshape(nc, nc)}
+        if need_h:
+            out["H"] = st[o:2 * o].reshape(nc, nc)
+            o *= 2
+        out["dpsi"], out["ll"], out["y2"] = st[o:o + nc], st[o + nc:o + 2 * nc], st[o + 2 * nc:o + 3 * nc]
+        return out
+
+    def eval_split(self, w, mu=None, density: DensityType = DensityType(), need_h: bool = False):
+        """pc_ctx_eval_loss then pc_ctx_eval_complete; returns (loss-only stats, kept, completed stats)."""
+        w = _c64(w)
+        nc = w.shape[0]
+        mu_a = _c64(mu) if mu is not None else None
+        n = (2 if need_h else 1) * nc * nc + 3 * nc
+        st = np.full(n, np.nan)
+        kept = C.c_int32()
+        err = _errbuf()
+        _raise(lib.pc_ctx_eval_loss(self.h, _ptr(w), nc, _ptr(mu_a) if mu_a is not None else None, density._c(),
+                                    1 if need_h else 0, _ptr(st), C.byref(kept), err, len(err)), err)
+        loss_only = st.copy()
+        if kept.value:
+            _raise(lib.pc_ctx_eval_complete(self.h, density._c(), 1 if need_h else 0, _ptr(st), err, len(err)), err)
+        return self._unpack(loss_only, nc, need_h), bool(kept.value), self._unpack(st, nc, need_h)
+
     def last_timing(self):
         k, c = C.c_double(), C.c_double()
         lib.pc_ctx_last_timing(self.h, C.byref(k), C.byref(c))
@@ -540,6 +569,13 @@ class DeviceContext:
         k, c, n = C.c_double(), C.c_double(), C.c_uint64()
         lib.pc_ctx_kernel_stats(self.h, C.byref(k), C.byref(c), C.byref(n), int(reset))
         return k.value, c.value, n.value
+
+    def kernel_breakdown(self, reset: bool = False) -> dict:
+        """{kind: (Σ kernel ms, launches)} for kind in fused / loss / fromy (HIP events)."""
+        ms = (C.c_double * 3)()
+        n = (C.c_uint64 * 3)()
+        lib.pc_ctx_kernel_breakdown(self.h, ms, n, int(reset))
+        return {k: (ms[i], n[i]) for i, k in enumerate(("fused", "loss", "fromy"))}
 
     def rowsum(self) -> np.ndarray:
         out = np.empty(self.n_features)

@@ -24,6 +24,7 @@ void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double*
 int rccl_unique_id(char* out);
 void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, uint64_t* n, int reset);
 void device_synchronize(int device);
+void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset);
 }  // namespace pcamd
 
 using namespace pcamd;
@@ -308,6 +309,26 @@ int pc_ctx_eval(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_de
   });
 }
 
+int pc_ctx_eval_loss(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density d, uint32_t flags,
+                     double* stats, int32_t* kept, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
+    if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
+    const bool h = (flags & PC_EVAL_NEED_H) != 0;
+    EvalStats st;
+    *kept = c->ev->eval_loss(w, nc, mu, d, h, &st) ? 1 : 0;
+    const size_t off = *kept ? st.buf.size() - 2 * nc : 0;  // kept: only [Σℓ | Σy²] are written
+    std::memcpy(stats + off, st.buf.data() + off, (st.buf.size() - off) * sizeof(double));
+  });
+}
+
+int pc_ctx_eval_complete(pc_ctx* c, pc_density d, uint32_t flags, double* stats, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    // only the entries [G | H | Σψ′] are written; Σℓ, Σy² of `stats` are left as they are
+    c->ev->eval_complete_into(d, (flags & PC_EVAL_NEED_H) != 0, stats);
+  });
+}
+
 int pc_ctx_rowsum(pc_ctx* c, double* out, char* err, size_t errlen) {
   return guarded(err, errlen, [&] { c->ev->rowsum(out); });
 }
@@ -330,6 +351,10 @@ void pc_ctx_last_timing(const pc_ctx* c, double* k, double* call) { device_ctx_t
 
 void pc_ctx_kernel_stats(pc_ctx* c, double* kernel_ms, double* call_ms, uint64_t* n, int32_t reset) {
   device_ctx_kernel_stats(c->ev.get(), kernel_ms, call_ms, n, reset);
+}
+
+void pc_ctx_kernel_breakdown(pc_ctx* c, double ms[3], uint64_t n[3], int32_t reset) {
+  device_ctx_kernel_breakdown(c->ev.get(), ms, n, reset);
 }
 
 int pc_device_synchronize(int32_t device) {

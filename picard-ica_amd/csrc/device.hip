@@ -164,6 +164,25 @@ __device__ __forceinline__ void density_eval(double y, double alpha, double inv_
   }
 }
 
+// ℓ(y) alone (line-search tries only need Σℓ; core.rs:73-82)
+template <int DENS>
+__device__ __forceinline__ double density_loss(double y, double alpha, double inv_alpha) {
+  if constexpr (DENS == DENS_TANH) {
+    double em_r, sc;
+    fm::exp_parts(fmax(-2.0 * fabs(alpha * y), -708.0), em_r, sc);
+    return fabs(y) + fm::log_1_2(2.0 + __builtin_fma(sc, em_r, sc - 1.0)) * inv_alpha;
+  } else if constexpr (DENS == DENS_EXP) {
+    double em_r, sc;
+    fm::exp_parts(fmax(-alpha / 2.0 * (y * y), -708.0), em_r, sc);
+    return -__builtin_fma(sc, em_r, sc) * inv_alpha;
+  } else if constexpr (DENS == DENS_CUBE) {
+    const double y2 = y * y;
+    return y2 * y2 / 4.0;
+  } else {
+    return 0.0;
+  }
+}
+
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -412,6 +431,259 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split evaluation for line-search tries (bit-identical sums to k_eval_fused):
+//   k_eval_loss  — Y stage + Σℓ, Σy² only (half the MFMA work, no ψ/ψ′), and
+//                  optionally Y written to HBM in MFMA-fragment order;
+//   k_eval_fromy — reads that Y back (coalesced 512-B fragments), ψ, ψ′ and
+//                  the G (H) stage: the rest of the statistics of an accepted try.
+// A rejected try then costs ≈ half a fused pass.
+// ---------------------------------------------------------------------------
+template <int NB, int DENS, bool STORE>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf,
+            const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
+            uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials, double* __restrict__ ybuf) {
+  using S = FusedShape<NB>;
+  constexpr int TS = S::TS, TB = S::TB, NCP = S::NCP;
+  constexpr int NFP = 16 * NB, KS = NFP / 4, XS = TS * NFP * 16, N2 = XS / 2, PRE = N2 / FUSED_THREADS;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int yi = wave % NB, yts = wave / NB;
+  const double inv_alpha = 1.0 / alpha;
+  extern __shared__ double smem[];
+  double* xs0 = smem;  // [2][TS][NFP][16]
+  double wf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) wf[ks] = Wp[(yi * 16 + lr) * NFP + 4 * ks + lk];
+  double rs_ll = 0.0, rs_y2 = 0.0;
+  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint64_t b_last = b_end - 1;
+  int xk[PRE], xt[PRE];
+  double xmu[PRE];
+  bool xrow_ok[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) {
+    const int e = tid + p * FUSED_THREADS;
+    xk[p] = e / (TB / 2);
+    xt[p] = 2 * (e % (TB / 2));
+    xrow_ok[p] = xk[p] < nf;
+    xmu[p] = (xrow_ok[p] && mu) ? mu[xk[p]] : 0.0;
+  }
+  double2 pre[PRE];
+  auto load_x = [&](uint64_t b) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p)
+      pre[p] = *reinterpret_cast<const double2*>(X + (size_t)(xrow_ok[p] ? xk[p] : 0) * ldx + b * TB + xt[p]);
+  };
+  auto store_x = [&](uint64_t b, double* xs) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      const uint64_t tg = b * TB + xt[p];
+      double2 v;
+      v.x = (xrow_ok[p] && tg < n_local) ? pre[p].x - xmu[p] : 0.0;
+      v.y = (xrow_ok[p] && tg + 1 < n_local) ? pre[p].y - xmu[p] : 0.0;
+      *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
+    }
+  };
+  auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
+  if (b_begin < b_end) {
+    load_x(b_begin);
+    store_x(b_begin, xs0);
+    load_x(clampb(b_begin + 1));
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0};
+      const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
+#pragma unroll
+      for (int ks = 0; ks < KS; ks += 2) {
+        ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+        yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
+      }
+      const d4 yv = ya + yb;
+      store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
+      load_x(clampb(b + 2));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double y = yv[r];
+        const double ll = density_loss<DENS>(y, alpha, inv_alpha);
+        rs_ll += (b * TB + yts * 16 + 4 * r + lk < n_local) ? ll : 0.0;
+        rs_y2 += y * y;
+        if constexpr (STORE) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = y;
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  rs_ll += __shfl_xor(rs_ll, 16); rs_ll += __shfl_xor(rs_ll, 32);
+  rs_y2 += __shfl_xor(rs_y2, 16); rs_y2 += __shfl_xor(rs_y2, 32);
+  double* rsb = xs0;  // [TS][NCP][2]
+  if (lk == 0) {
+    rsb[(yts * NCP + yi * 16 + lr) * 2 + 0] = rs_ll;
+    rsb[(yts * NCP + yi * 16 + lr) * 2 + 1] = rs_y2;
+  }
+  __syncthreads();
+  double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ | Σy²]
+  for (int e = tid; e < NCP * 2; e += FUSED_THREADS) {
+    const int row = e / 2, c = e % 2;
+    double sum = 0.0;
+    for (int ts = 0; ts < TS; ++ts) sum += rsb[(ts * NCP + row) * 2 + c];
+    out[c * NCP + row] = sum;
+  }
+}
+
+template <int NB, bool NEED_H, int DENS>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, uint64_t bpw, uint64_t n_blocks,
+             double* __restrict__ partials) {
+  using S = FusedShape<NB>;
+  constexpr int TS = S::TS, TB = S::TB, NCP = S::NCP, KKW = S::KKW, GI = S::GI, GJ = S::GJ;
+  constexpr int NIMG = NEED_H ? 3 : 2;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int yi = wave % NB, yts = wave / NB;
+  const double inv_alpha = 1.0 / alpha;
+  extern __shared__ double smem[];
+  double* img0 = smem;  // [2][NIMG][KK][NB][64]
+  int gi0, gj0, kk0;
+  if constexpr (NB == 8) { gi0 = (wave >> 2) * 4; gj0 = (wave & 3) * 2; kk0 = 0; }
+  else if constexpr (NB == 4) { gi0 = wave >> 1; gj0 = (wave & 1) * 2; kk0 = 0; }
+  else if constexpr (NB == 2) { gi0 = (wave & 3) >> 1; gj0 = wave & 1; kk0 = (wave >> 2) * KKW; }
+  else { gi0 = 0; gj0 = 0; kk0 = wave * KKW; }
+  d4 accg[GI][GJ];
+  d4 acch[GI][GJ];
+#pragma unroll
+  for (int i = 0; i < GI; ++i)
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
+  double rs_dpsi = 0.0;
+  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint64_t b_last = b_end - 1;
+  auto load_y = [&](uint64_t b) {
+    d4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = ybuf[((b * 8 + wave) * 4 + r) * 64 + lane];
+    return v;
+  };
+  auto elementwise = [&](const d4& yv, uint64_t b, double* img) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double y = yv[r];
+      double psi, dpsi, ll;
+      density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
+      (void)ll;
+      rs_dpsi += (b * TB + yts * 16 + 4 * r + lk < n_local) ? dpsi : 0.0;
+      const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
+      img[f] = psi;
+      img[S::FRAGS + f] = y;
+      if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi;
+    }
+  };
+  auto g_stage = [&](const double* img) {
+#pragma unroll
+    for (int q = 0; q < KKW; ++q) {
+      const int kk = kk0 + q;
+      double pa[GI], yf[GJ];
+#pragma unroll
+      for (int i = 0; i < GI; ++i) pa[i] = img[(kk * NB + gi0 + i) * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < GJ; ++j) yf[j] = img[S::FRAGS + (kk * NB + gj0 + j) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < GI; ++i)
+#pragma unroll
+        for (int j = 0; j < GJ; ++j) accg[i][j] = mfma(pa[i], yf[j], accg[i][j]);
+      if constexpr (NEED_H) {
+#pragma unroll
+        for (int i = 0; i < GI; ++i) {
+          const double da = img[2 * S::FRAGS + (kk * NB + gi0 + i) * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < GJ; ++j) acch[i][j] = mfma(da, yf[j] * yf[j], acch[i][j]);
+        }
+      }
+    }
+  };
+  if (b_begin < b_end) {
+    auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
+    elementwise(load_y(b_begin), b_begin, img0);
+    d4 pre = load_y(clampb(b_begin + 1));
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_last; ++b) {
+      const d4 yv = pre;
+      pre = load_y(clampb(b + 2));
+      g_stage(img0 + cur * NIMG * S::FRAGS);
+      elementwise(yv, b + 1, img0 + (cur ^ 1) * NIMG * S::FRAGS);
+      __syncthreads();
+      cur ^= 1;
+    }
+    g_stage(img0 + cur * NIMG * S::FRAGS);
+    __syncthreads();
+  }
+  double* out = partials + (size_t)blockIdx.x * fused_partial_stride(NCP, NEED_H);
+  double* red = img0;
+  if constexpr (S::KSPL == 1) {
+#pragma unroll
+    for (int i = 0; i < GI; ++i)
+#pragma unroll
+      for (int j = 0; j < GJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (gi0 + i) * 16 + lk + 4 * r, col = (gj0 + j) * 16 + lr;
+          out[row * NCP + col] = accg[i][j][r];
+          if constexpr (NEED_H) out[NCP * NCP + row * NCP + col] = acch[i][j][r];
+        }
+  } else {
+    constexpr int NBLK = NB * NB;
+    const int blk = gi0 * NB + gj0;
+    const int sp = kk0 / KKW;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[(sp * NBLK + blk) * 256 + r * 64 + lane] = accg[0][0][r];
+      if constexpr (NEED_H) red[(S::KSPL + sp) * NBLK * 256 + blk * 256 + r * 64 + lane] = acch[0][0][r];
+    }
+    __syncthreads();
+    if (sp == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double g = 0.0, h = 0.0;
+        for (int s2 = 0; s2 < S::KSPL; ++s2) {
+          g += red[(s2 * NBLK + blk) * 256 + r * 64 + lane];
+          if constexpr (NEED_H) h += red[(S::KSPL + s2) * NBLK * 256 + blk * 256 + r * 64 + lane];
+        }
+        const int row = gi0 * 16 + lk + 4 * r, col = gj0 * 16 + lr;
+        out[row * NCP + col] = g;
+        if constexpr (NEED_H) out[NCP * NCP + row * NCP + col] = h;
+      }
+    }
+    __syncthreads();
+  }
+  rs_dpsi += __shfl_xor(rs_dpsi, 16); rs_dpsi += __shfl_xor(rs_dpsi, 32);
+  double* rsb = img0 + 2 * NIMG * S::FRAGS - TS * NCP;  // [TS][NCP] at the end of the image area
+  __syncthreads();
+  if (lk == 0) rsb[yts * NCP + yi * 16 + lr] = rs_dpsi;
+  __syncthreads();
+  double* orow = out + (size_t)(NEED_H ? 2 : 1) * NCP * NCP;
+  for (int row = tid; row < NCP; row += FUSED_THREADS) {
+    double sum = 0.0;
+    for (int ts = 0; ts < TS; ++ts) sum += rsb[ts * NCP + row];
+    orow[row] = sum;
+  }
+}
+
+// out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets (fixed order)
+__global__ void k_reduce_rows(const double* __restrict__ partials, int nwg, size_t pstride, size_t poff, int ncp,
+                              int nc, int nsets, double* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nsets * nc) return;
+  const int c = e / nc, row = e % nc;
+  double s = 0.0;
+  for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + poff + (size_t)c * ncp + row];
+  out[e] = s;
+}
+
 // Fixed-order sum of per-workgroup partials into the compact stats layout
 // [G nc×nc | H nc×nc | Σψ′ nc | Σℓ nc | Σy² nc].
 __global__ void k_reduce(const double* __restrict__ partials, int nwg, size_t pstride, int ncp, int nc,
@@ -655,6 +927,10 @@ struct DeviceCtx : Evaluator {
   double* d_part = nullptr; size_t cap_part = 0;
   double* d_stats = nullptr; size_t cap_stats = 0;
   double* d_chunk = nullptr; size_t cap_chunk = 0;
+  double* d_ybuf = nullptr; size_t cap_ybuf = 0;
+  bool ybuf_failed = false;
+  // state of the last split (loss-only) evaluation whose Y is kept in d_ybuf
+  size_t kept_nc = 0; int kept_nb = 0;
   hipEvent_t ev[4];
   double last_kernel_ms = 0, last_call_ms = 0;
   double sum_kernel_ms = 0, sum_call_ms = 0;
@@ -677,7 +953,7 @@ struct DeviceCtx : Evaluator {
   ~DeviceCtx() override {
     (void)hipSetDevice(device);
     if (comm) ncclCommDestroy(comm);
-    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk})
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf})
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -915,6 +1191,194 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
   }
 
+  // ---- split line-search evaluation -------------------------------------
+  bool fused_ok(size_t nc, int dens, double alpha, bool need_h) const {
+    const int nb = pick_nb(nc);
+    return nb > 0 && nf <= (uint64_t)(16 * nb) && !(need_h && nb == 8) &&
+           !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0)) && dens != DENS_LINEAR;
+  }
+  // d_ybuf sized for Y of this shard in fragment order; false if HBM is short
+  bool ensure_ybuf(int nb) {
+    const int tb = 16 * (8 / nb);
+    const uint64_t nblk = (n_local_ + tb - 1) / tb;
+    const size_t need = (size_t)nblk * 16 * nb * tb;
+    if (need <= cap_ybuf) return true;
+    if (ybuf_failed) return false;
+    size_t fr = 0, tot = 0;
+    HIP_OK(hipMemGetInfo(&fr, &tot));
+    if (d_ybuf) { HIP_OK(hipFree(d_ybuf)); fr += cap_ybuf * sizeof(double); d_ybuf = nullptr; cap_ybuf = 0; }
+    if (need * sizeof(double) + (size_t(2) << 30) > fr || hipMalloc(&d_ybuf, need * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      d_ybuf = nullptr;
+      ybuf_failed = true;
+      return false;
+    }
+    cap_ybuf = need;
+    return true;
+  }
+
+  template <int NB, int D>
+  void launch_loss(const double* dmu, double alpha, bool store, double* st_rows) {
+    using S = FusedShape<NB>;
+    const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
+    int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_blocks, 1));
+    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
+    nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * S::NCP);
+    const size_t lds = (size_t)2 * S::TS * 16 * NB * 16 * sizeof(double);
+    HIP_OK(hipEventRecord(ev[1], stream));
+    if (store) {
+      k_eval_loss<NB, D, true><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw,
+                                                                    n_blocks, part, d_ybuf);
+    } else {
+      k_eval_loss<NB, D, false><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha,
+                                                                     bpw, n_blocks, part, nullptr);
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    k_reduce_rows<<<1, 512, 0, stream>>>(part, nwg, 2 * S::NCP, 0, S::NCP, (int)kept_nc_pending, 2, st_rows);
+    HIP_OK(hipGetLastError());
+  }
+  size_t kept_nc_pending = 0;
+
+  template <int NB, bool H, int D>
+  void launch_fromy(double alpha, double* st) {
+    using S = FusedShape<NB>;
+    const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
+    int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_blocks, 1));
+    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
+    nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    const size_t pstride = fused_partial_stride(S::NCP, H);
+    double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
+    const size_t lds = (size_t)2 * (H ? 3 : 2) * S::FRAGS * sizeof(double);
+    HIP_OK(hipEventRecord(ev[1], stream));
+    k_eval_fromy<NB, H, D><<<nwg, FUSED_THREADS, lds, stream>>>(d_ybuf, n_local_, alpha, bpw, n_blocks, part);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    const size_t nc = kept_nc;
+    const size_t e1 = (H ? 2 : 1) * nc * nc + nc;  // [G | H | Σψ′]
+    k_reduce<<<(e1 + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st);
+    HIP_OK(hipGetLastError());
+  }
+
+  double sum_loss_ms = 0, sum_fromy_ms = 0;
+  uint64_t n_loss = 0, n_fromy = 0;
+  void finish_timing(bool kernel_timed, int kind = 0) {
+    HIP_OK(hipEventRecord(ev[3], stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    float a = 0, b = 0;
+    if (kernel_timed) HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2]));
+    HIP_OK(hipEventElapsedTime(&b, ev[0], ev[3]));
+    last_kernel_ms = kernel_timed ? a : b;
+    last_call_ms = b;
+    sum_call_ms += b;
+    if (kernel_timed) { sum_split_ms += a; ++n_split; }
+    if (kind == 1) { sum_loss_ms += a; ++n_loss; }
+    if (kind == 2) { sum_fromy_ms += a; ++n_fromy; }
+  }
+  double sum_split_ms = 0;
+  uint64_t n_split = 0;
+
+  bool eval_loss(const double* w, size_t nc, const double* mu, pc_density d, bool need_h, EvalStats* out) override {
+    if (!fused_ok(nc, d.kind, d.alpha, need_h)) {
+      eval(w, nc, mu, d, need_h, out);
+      return false;
+    }
+    HIP_OK(hipSetDevice(device));
+    const int nb = pick_nb(nc);
+    const int nfp = 16 * nb;
+    const bool store = ensure_ybuf(nb);
+    if (!store) {  // no room to keep Y: a complete pass instead
+      eval(w, nc, mu, d, need_h, out);
+      return false;
+    }
+    out->nc = nc;
+    out->has_h = need_h;
+    out->buf.assign(EvalStats::size(nc, need_h), 0.0);
+    const size_t total = EvalStats::size(nc, need_h);
+    double* st = ensure(d_stats, cap_stats, total);
+    double* st_rows = st + total - 2 * nc;  // [Σℓ | Σy²] are the last 2·nc entries
+    HIP_OK(hipEventRecord(ev[0], stream));
+    double* dmu = nullptr;
+    if (mu) {
+      dmu = ensure(d_mu, cap_mu, std::max<size_t>(nfp, nf));
+      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    }
+    std::vector<double> wp((size_t)16 * nb * nfp, 0.0);
+    for (size_t i = 0; i < nc; ++i)
+      for (size_t k = 0; k < nf; ++k) wp[i * nfp + k] = w[i * nf + k];
+    ensure(d_w, cap_w, wp.size());
+    HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    kept_nc_pending = nc;
+#define PC_LOSS(NBV)                                                                            \
+  switch (d.kind) {                                                                             \
+    case DENS_TANH: launch_loss<NBV, DENS_TANH>(dmu, d.alpha, store, st_rows); break;            \
+    case DENS_EXP: launch_loss<NBV, DENS_EXP>(dmu, d.alpha, store, st_rows); break;              \
+    default: launch_loss<NBV, DENS_CUBE>(dmu, d.alpha, store, st_rows); break;                   \
+  }
+    switch (nb) {
+      case 1: PC_LOSS(1); break;
+      case 2: PC_LOSS(2); break;
+      case 4: PC_LOSS(4); break;
+      default: PC_LOSS(8); break;
+    }
+#undef PC_LOSS
+    allreduce(st_rows, 2 * nc);
+    HIP_OK(hipMemcpyAsync(out->buf.data() + total - 2 * nc, st_rows, 2 * nc * sizeof(double),
+                          hipMemcpyDeviceToHost, stream));
+    finish_timing(true, 1);
+    kept_nc = nc;
+    kept_nb = nb;
+    return true;
+  }
+
+  void eval_complete_into(pc_density d, bool need_h, double* stats) override {
+    if (kept_nc == 0) throw computation_error("no kept evaluation to complete");
+    EvalStats tmp;
+    tmp.nc = kept_nc;
+    tmp.has_h = need_h;
+    tmp.buf.assign(EvalStats::size(kept_nc, need_h), 0.0);
+    eval_complete(d, need_h, &tmp);
+    const size_t e1 = (need_h ? 2 : 1) * kept_nc * kept_nc + kept_nc;
+    std::memcpy(stats, tmp.buf.data(), e1 * sizeof(double));
+  }
+
+  void eval_complete(pc_density d, bool need_h, EvalStats* out) override {
+    HIP_OK(hipSetDevice(device));
+    const size_t nc = kept_nc;
+    const size_t total = EvalStats::size(nc, need_h);
+    double* st = ensure(d_stats, cap_stats, total);
+    const size_t e1 = (need_h ? 2 : 1) * nc * nc + nc;
+    HIP_OK(hipEventRecord(ev[0], stream));
+#define PC_FROMY(NBV)                                                                             \
+  if (need_h) {                                                                                   \
+    switch (d.kind) {                                                                             \
+      case DENS_TANH: launch_fromy<NBV, true, DENS_TANH>(d.alpha, st); break;                    \
+      case DENS_EXP: launch_fromy<NBV, true, DENS_EXP>(d.alpha, st); break;                      \
+      default: launch_fromy<NBV, true, DENS_CUBE>(d.alpha, st); break;                           \
+    }                                                                                             \
+  } else {                                                                                        \
+    switch (d.kind) {                                                                             \
+      case DENS_TANH: launch_fromy<NBV, false, DENS_TANH>(d.alpha, st); break;                   \
+      case DENS_EXP: launch_fromy<NBV, false, DENS_EXP>(d.alpha, st); break;                     \
+      default: launch_fromy<NBV, false, DENS_CUBE>(d.alpha, st); break;                          \
+    }                                                                                             \
+  }
+    switch (kept_nb) {
+      case 1: PC_FROMY(1); break;
+      case 2: PC_FROMY(2); break;
+      case 4: PC_FROMY(4); break;
+      default:
+        if (need_h) throw computation_error("split evaluation with H needs nc <= 64");
+        PC_FROMY(8);
+        break;
+    }
+#undef PC_FROMY
+    allreduce(st, e1);
+    HIP_OK(hipMemcpyAsync(out->buf.data(), st, e1 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    finish_timing(true, 2);
+  }
+
   void sources(const double* w, size_t nc, const double* mu, double* out) override {
     HIP_OK(hipSetDevice(device));
     double* dw = ensure(d_w, cap_w, nc * nf);
@@ -1001,6 +1465,16 @@ void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, u
   *call_ms = d->sum_call_ms;
   *n = d->n_kernel;
   if (reset) { d->sum_kernel_ms = 0; d->sum_call_ms = 0; d->n_kernel = 0; }
+}
+void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset) {
+  auto* d = static_cast<DeviceCtx*>(e);
+  ms[0] = d->sum_kernel_ms; n[0] = d->n_kernel;
+  ms[1] = d->sum_loss_ms; n[1] = d->n_loss;
+  ms[2] = d->sum_fromy_ms; n[2] = d->n_fromy;
+  if (reset) {
+    d->sum_kernel_ms = d->sum_loss_ms = d->sum_fromy_ms = d->sum_split_ms = d->sum_call_ms = 0;
+    d->n_kernel = d->n_loss = d->n_fromy = d->n_split = 0;
+  }
 }
 void device_synchronize(int device) {
   HIP_OK(hipSetDevice(device));

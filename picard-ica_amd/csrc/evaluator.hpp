@@ -57,6 +57,21 @@ class Evaluator {
   virtual void sources(const double* w, size_t nc, const double* mu, double* out) = 0;
   virtual uint64_t n_local() const = 0;
   virtual void moments4(const double* w, size_t nc, const double* mu, double* out) = 0;
+  // Line-search try (core.rs:124-127 only needs Σℓ, Σy²). May compute just
+  // those and keep Y on the device; returns true in that case, and then
+  // eval_complete fills G (H) and Σψ′ of the SAME W from the kept Y. A
+  // device that cannot split falls back to a full pass and returns false.
+  virtual bool eval_loss(const double* w, size_t nc, const double* mu, pc_density d, bool need_h,
+                         EvalStats* out) {
+    eval(w, nc, mu, d, need_h, out);
+    return false;
+  }
+  virtual void eval_complete(pc_density d, bool need_h, EvalStats* out) { (void)d; (void)need_h; (void)out; }
+  // eval_complete into a raw packed stats buffer (C ABI)
+  virtual void eval_complete_into(pc_density d, bool need_h, double* stats) {
+    (void)d; (void)need_h; (void)stats;
+    throw computation_error("no kept evaluation to complete");
+  }
 };
 
 }  // namespace pcamd

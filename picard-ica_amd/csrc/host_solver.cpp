@@ -215,6 +215,19 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   ++total_evals_;
 }
 
+bool Solver::evaluate_loss(const Mat& w_core, EvalStats* out) {
+  Mat wt = matmul(w_core, P_);
+  const bool partial = ev_->eval_loss(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
+  ++last_evals_;
+  ++total_evals_;
+  return partial;
+}
+
+void Solver::complete(EvalStats* out) {
+  ev_->eval_complete(cfg_.density, !cfg_.ortho, out);
+  ++total_completions_;
+}
+
 // core.rs:39-85 + loss_to_f64 core.rs:90-96, from the pass's per-row sums
 double Solver::loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular) {
   const double t = (double)T_;
@@ -266,10 +279,13 @@ void Solver::init_core() {  // core.rs:175-209
 }
 
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries) {  // core.rs:99-150
+  // Evaluation schedule (results are bit-identical either way): a try is a
+  // full fused pass, or a loss-only pass whose Y stays on the device and is
+  // completed (G, H, Σψ′) only if that try becomes the new iterate.
   const size_t n = nc_;
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
-  LsResult r{false, W_, S_, current_loss_, Mat()};
+  LsResult r{false, W_, S_, current_loss_, Mat(), false, 0};
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
@@ -279,7 +295,13 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries) {  // c
       for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += alpha * direction.a[e];
     }
     r.w = matmul(transform, W_);
-    evaluate(r.w, &r.stats);
+    if (k == 0 && first_full_) {
+      evaluate(r.w, &r.stats);
+      r.partial = false;
+    } else {
+      r.partial = evaluate_loss(r.w, &r.stats);
+    }
+    r.tries = k + 1;
     bool singular;
     r.loss = loss_of(r.stats, r.w, signs_, &singular);
     if (r.loss < current_loss_) {
@@ -378,10 +400,12 @@ bool Solver::step() {
   }
   Mat direction = compute_direction(g, h, h_off, mem_, ortho);  // core.rs:334
   LsResult res = line_search(direction, cfg_.ls_tries);
+  first_full_ = res.success && res.tries == 1;
   if (!res.success) {  // core.rs:349-364
     mem_.clear();
     res = line_search(scale(g, -1.0), 10);
   }
+  if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;
   W_ = std::move(res.w);

@@ -34,11 +34,14 @@ class Solver {
   double last_gnorm() const { return gradient_norm_; }
   uint64_t last_evals() const { return last_evals_; }
   uint64_t total_evals() const { return total_evals_; }
+  uint64_t total_completions() const { return total_completions_; }
 
  private:
   double loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular);
   void evaluate(const Mat& w_core, EvalStats* out);
-  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; };
+  bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
+  void complete(EvalStats* out);
+  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; };
   LsResult line_search(const Mat& direction, size_t tries);
   void init_core();
   Mat ica_par(const Mat& w_init);
@@ -72,6 +75,10 @@ class Solver {
   double gradient_norm_ = 1.0;
   bool converged_ = false, done_ = false;
   uint64_t last_evals_ = 0, total_evals_ = 0;
+  uint64_t total_completions_ = 0;
+  // first try of a line search as a full fused pass while first tries keep
+  // being accepted; otherwise loss-only tries + one completion pass
+  bool first_full_ = true;
 };
 
 }  // namespace pcamd

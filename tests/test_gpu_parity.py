@@ -77,6 +77,25 @@ def test_eval_no_mean_and_tiny_t(pa, po, rng):
             assert rel_err(got[k], want[k]) <= TOL, (t, k)
 
 
+@pytest.mark.parametrize("n", [8, 30, 64, 128])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
+@pytest.mark.parametrize("need_h", [False, True])
+def test_split_eval_bit_identical(pa, rng, n, dens, need_h):
+    """Loss-only try + completion from the kept Y == one fused pass, bit for bit."""
+    x = laplace_mix(rng, n, 4099)
+    ctx = ctx_with(pa, x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = pa.DensityType(["tanh", "exp", "cube"].index(dens[0]), dens[1])
+    full = ctx.eval(w, mu, d, need_h)
+    loss_only, kept, done = ctx.eval_split(w, mu, d, need_h)
+    assert np.array_equal(loss_only["ll"], full["ll"]) and np.array_equal(loss_only["y2"], full["y2"])
+    if kept:
+        assert np.isnan(loss_only["G"]).all()
+    for k in full:
+        assert np.array_equal(done[k], full[k]), k
+
+
 def test_eval_deterministic(pa, rng):
     x = laplace_mix(rng, 64, 20000)
     ctx = ctx_with(pa, x)
