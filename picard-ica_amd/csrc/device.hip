@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1202,6 +1203,7 @@ struct DeviceCtx : Evaluator {
     const int tb = 16 * (8 / nb);
     const uint64_t nblk = (n_local_ + tb - 1) / tb;
     const size_t need = (size_t)nblk * 16 * nb * tb;
+    if (std::getenv("PICARD_NO_YSTORE")) return false;  // experiment knob: never keep Y
     if (need <= cap_ybuf) return true;
     if (ybuf_failed) return false;
     size_t fr = 0, tot = 0;

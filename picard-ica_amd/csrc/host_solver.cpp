@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -205,6 +206,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
     std::printf("Running Picard...\n");
     std::fflush(stdout);
   }
+  trace_ = std::getenv("PICARD_TRACE") != nullptr;
   init_core();
 }
 
@@ -400,12 +402,19 @@ bool Solver::step() {
   }
   Mat direction = compute_direction(g, h, h_off, mem_, ortho);  // core.rs:334
   LsResult res = line_search(direction, cfg_.ls_tries);
+  const size_t first_tries = res.tries;
+  const bool first_ok = res.success;
   first_full_ = res.success && res.tries == 1;
   if (!res.success) {  // core.rs:349-364
     mem_.clear();
     res = line_search(scale(g, -1.0), 10);
   }
   if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
+  if (trace_) {
+    std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d\n",
+                 iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
+                 res.partial ? 1 : 0);
+  }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;
   W_ = std::move(res.w);

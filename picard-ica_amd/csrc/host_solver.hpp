@@ -79,6 +79,7 @@ class Solver {
   // first try of a line search as a full fused pass while first tries keep
   // being accepted; otherwise loss-only tries + one completion pass
   bool first_full_ = true;
+  bool trace_ = false;  // PICARD_TRACE=1: one stderr line per iteration (line-search tries)
 };
 
 }  // namespace pcamd
