@@ -117,6 +117,22 @@ __device__ __forceinline__ double log_1_2(double z) {
 // ℓ = |y| + ln(1 + e^{−2α|y|})/α = |y| + ln(2 + em)/α  (α > 0).
 // inv_alpha = 1/α is precomputed (the reference divides; ≤ 1 ulp apart).
 // ---------------------------------------------------------------------------
+// Shared by every kernel so ℓ, ψ′ and y² are bit-identical across the fused,
+// loss-only and completion passes (device code is built with -ffp-contract=on).
+__device__ __forceinline__ double tanh_em(double y, double alpha) {  // e^{-2|αy|} − 1
+  double em_r, sc;
+  fm::exp_parts(fmax(-2.0 * fabs(alpha * y), -708.0), em_r, sc);
+  return __builtin_fma(sc, em_r, sc - 1.0);
+}
+__device__ __forceinline__ double tanh_ll(double y, double em, double inv_alpha) {
+  return __builtin_fma(fm::log_1_2(2.0 + em), inv_alpha, fabs(y));
+}
+__device__ __forceinline__ double exp_k(double y, double alpha) {  // e^{-α y²/2}
+  double em_r, sc;
+  fm::exp_parts(fmax(-alpha / 2.0 * (y * y), -708.0), em_r, sc);
+  return __builtin_fma(sc, em_r, sc);
+}
+
 template <int DENS, bool FAST>
 __device__ __forceinline__ void density_eval(double y, double alpha, double inv_alpha, double& psi, double& dpsi,
                                              double& ll) {
@@ -124,14 +140,11 @@ __device__ __forceinline__ void density_eval(double y, double alpha, double inv_
     const double ay = fabs(y);
     const double a = alpha * y;
     if constexpr (FAST) {  // α > 0 (checked on the host)
-      double em_r, sc;
-      fm::exp_parts(fmax(-2.0 * fabs(a), -708.0), em_r, sc);
-      const double em = __builtin_fma(sc, em_r, sc - 1.0);  // e^{-2|a|} − 1 ∈ (−1, 0]
-      const double z = 2.0 + em;                            // 1 + e^{-2α|y|} ∈ (1, 2]
-      const double th = copysign(fm::div_nr(-em, z), a);
+      const double em = tanh_em(y, alpha);  // e^{-2|a|} − 1 ∈ (−1, 0]; 2 + em = 1 + e^{-2α|y|} ∈ (1, 2]
+      const double th = copysign(fm::div_nr(-em, 2.0 + em), a);
       psi = th;
-      dpsi = alpha * (1.0 - th * th);
-      ll = ay + fm::log_1_2(z) * inv_alpha;
+      dpsi = alpha * __builtin_fma(-th, th, 1.0);
+      ll = tanh_ll(y, em, inv_alpha);
     } else {
       const double th = tanh(a);
       psi = th;
@@ -143,9 +156,8 @@ __device__ __forceinline__ void density_eval(double y, double alpha, double inv_
     const double x = -alpha / 2.0 * y2;
     double k;
     if constexpr (FAST) {  // α > 0: x ≤ 0
-      double em_r, sc;
-      fm::exp_parts(fmax(x, -708.0), em_r, sc);
-      k = __builtin_fma(sc, em_r, sc);
+      (void)x;
+      k = exp_k(y, alpha);
       ll = -k * inv_alpha;
     } else {
       k = exp(x);
@@ -169,13 +181,9 @@ __device__ __forceinline__ void density_eval(double y, double alpha, double inv_
 template <int DENS>
 __device__ __forceinline__ double density_loss(double y, double alpha, double inv_alpha) {
   if constexpr (DENS == DENS_TANH) {
-    double em_r, sc;
-    fm::exp_parts(fmax(-2.0 * fabs(alpha * y), -708.0), em_r, sc);
-    return fabs(y) + fm::log_1_2(2.0 + __builtin_fma(sc, em_r, sc - 1.0)) * inv_alpha;
+    return tanh_ll(y, tanh_em(y, alpha), inv_alpha);
   } else if constexpr (DENS == DENS_EXP) {
-    double em_r, sc;
-    fm::exp_parts(fmax(-alpha / 2.0 * (y * y), -708.0), em_r, sc);
-    return -__builtin_fma(sc, em_r, sc) * inv_alpha;
+    return -exp_k(y, alpha) * inv_alpha;
   } else if constexpr (DENS == DENS_CUBE) {
     const double y2 = y * y;
     return y2 * y2 / 4.0;
@@ -213,7 +221,7 @@ __host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
 }
 
 // Software-pipelined over blocks with ONE barrier per block: iteration b
-// runs the Y stage of block b+1 (two interleaved MFMA chains) next to the G
+// runs the Y stage of block b+1 (four interleaved MFMA chains) next to the G
 // stage of block b (GI·GJ independent accumulators) in one basic block, so
 // the chains' latency hides under independent MFMAs; X tiles and ψ/Y images
 // are double-buffered. Loads/stores of X use clamped block indices and
@@ -295,15 +303,23 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     }
   };
   // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over NFP, as two chains
+  // (same four-chain order as k_eval_loss, so both produce bit-identical Y)
   auto y_stage = [&](const double* xs) {
-    d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0};
+    d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0}, yc = d4{0, 0, 0, 0}, yd = d4{0, 0, 0, 0};
     const double* xrow = xs + (yts * NFP + lk) * 16 + lr;
+    if constexpr (KS >= 4) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ks += 2) {
-      ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
-      yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
+      for (int ks = 0; ks < KS; ks += 4) {
+        ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+        yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
+        yc = mfma(xrow[(4 * ks + 8) * 16], wf[ks + 2], yc);
+        yd = mfma(xrow[(4 * ks + 12) * 16], wf[ks + 3], yd);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
     }
-    return ya + yb;
+    return (ya + yb) + (yc + yd);
   };
   // density on the tile, row sums, hand-off of the ψ / y (/ ψ′) fragments
   auto elementwise = [&](const d4& yv, uint64_t b, double* img) {
@@ -315,7 +331,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       const bool valid = b * TB + yts * 16 + 4 * r + lk < n_local;
       rs_dpsi += valid ? dpsi : 0.0;
       rs_ll += valid ? ll : 0.0;
-      rs_y2 += y * y;  // y = 0 exactly for samples past the end (zero X columns)
+      rs_y2 = __builtin_fma(y, y, rs_y2);  // y = 0 exactly for samples past the end (zero X columns)
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
       img[f] = psi;
       img[S::FRAGS + f] = y;
@@ -441,7 +457,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 // A rejected try then costs ≈ half a fused pass.
 // ---------------------------------------------------------------------------
 template <int NB, int DENS, bool STORE>
-__global__ void __launch_bounds__(FUSED_THREADS, 2)
+__global__ void __launch_bounds__(FUSED_THREADS, 4)
 k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf,
             const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
             uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials, double* __restrict__ ybuf) {
@@ -496,14 +512,22 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
     __syncthreads();
     int cur = 0;
     for (uint64_t b = b_begin; b < b_end; ++b) {
-      d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0};
+      // four independent chains: no G stage here to hide the MFMA latency behind
+      d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0}, yc = d4{0, 0, 0, 0}, yd = d4{0, 0, 0, 0};
       const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
+      if constexpr (KS >= 4) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ks += 2) {
-        ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
-        yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
+        for (int ks = 0; ks < KS; ks += 4) {
+          ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+          yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
+          yc = mfma(xrow[(4 * ks + 8) * 16], wf[ks + 2], yc);
+          yd = mfma(xrow[(4 * ks + 12) * 16], wf[ks + 3], yd);
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
       }
-      const d4 yv = ya + yb;
+      const d4 yv = (ya + yb) + (yc + yd);
       store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
       load_x(clampb(b + 2));
 #pragma unroll
@@ -511,7 +535,7 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
         const double y = yv[r];
         const double ll = density_loss<DENS>(y, alpha, inv_alpha);
         rs_ll += (b * TB + yts * 16 + 4 * r + lk < n_local) ? ll : 0.0;
-        rs_y2 += y * y;
+        rs_y2 = __builtin_fma(y, y, rs_y2);
         if constexpr (STORE) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = y;
       }
       __syncthreads();
@@ -536,7 +560,7 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
 }
 
 template <int NB, bool NEED_H, int DENS>
-__global__ void __launch_bounds__(FUSED_THREADS, 2)
+__global__ void __launch_bounds__(FUSED_THREADS, 4)
 k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, uint64_t bpw, uint64_t n_blocks,
              double* __restrict__ partials) {
   using S = FusedShape<NB>;
@@ -1070,15 +1094,25 @@ struct DeviceCtx : Evaluator {
     run_eval(w, nc, mu, d.kind, d.alpha, need_h, out->buf.data());
   }
 
+  // Block → workgroup partition shared by the fused, loss-only and completion
+  // kernels: identical partitions give identical summation orders, so the split
+  // evaluation is bit-identical to the fused pass. 2 workgroups per CU: the
+  // split kernels fit two (≤128 VGPRs), the fused one runs them in two rounds.
+  int partition(uint64_t n_blocks, uint64_t* bpw) const {
+    const uint64_t nb = std::max<uint64_t>(n_blocks, 1);
+    const uint64_t want = std::min<uint64_t>((uint64_t)2 * n_cu, nb);
+    *bpw = (nb + want - 1) / want;
+    return (int)((nb + *bpw - 1) / *bpw);
+  }
+
   static int pick_nb(size_t nc) { return nc <= 16 ? 1 : nc <= 32 ? 2 : nc <= 64 ? 4 : nc <= 128 ? 8 : 0; }
 
   template <int NB, bool H, int D>
   void launch_fused(int nfp, const double* dmu, double alpha, double* st, size_t nc) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
-    int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_blocks, 1));
-    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
-    nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    uint64_t bpw;
+    const int nwg = partition(n_blocks, &bpw);
     const size_t pstride = fused_partial_stride(S::NCP, H);
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
@@ -1223,9 +1257,8 @@ struct DeviceCtx : Evaluator {
   void launch_loss(const double* dmu, double alpha, bool store, double* st_rows) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
-    int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_blocks, 1));
-    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
-    nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    uint64_t bpw;
+    const int nwg = partition(n_blocks, &bpw);
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * S::NCP);
     const size_t lds = (size_t)2 * S::TS * 16 * NB * 16 * sizeof(double);
     HIP_OK(hipEventRecord(ev[1], stream));
@@ -1247,9 +1280,8 @@ struct DeviceCtx : Evaluator {
   void launch_fromy(double alpha, double* st) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
-    int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_blocks, 1));
-    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
-    nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    uint64_t bpw;
+    const int nwg = partition(n_blocks, &bpw);
     const size_t pstride = fused_partial_stride(S::NCP, H);
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)2 * (H ? 3 : 2) * S::FRAGS * sizeof(double);
@@ -1334,6 +1366,24 @@ struct DeviceCtx : Evaluator {
     return true;
   }
 
+  template <int NB>
+  void dispatch_fromy(pc_density d, bool need_h, double* st) {
+    if constexpr (NB == 8) {  // H at NB = 8 does not fit the register budget: never split (fused_ok)
+      if (need_h) throw computation_error("split evaluation with H needs nc <= 64");
+    } else if (need_h) {
+      switch (d.kind) {
+        case DENS_TANH: launch_fromy<NB, true, DENS_TANH>(d.alpha, st); return;
+        case DENS_EXP: launch_fromy<NB, true, DENS_EXP>(d.alpha, st); return;
+        default: launch_fromy<NB, true, DENS_CUBE>(d.alpha, st); return;
+      }
+    }
+    switch (d.kind) {
+      case DENS_TANH: launch_fromy<NB, false, DENS_TANH>(d.alpha, st); break;
+      case DENS_EXP: launch_fromy<NB, false, DENS_EXP>(d.alpha, st); break;
+      default: launch_fromy<NB, false, DENS_CUBE>(d.alpha, st); break;
+    }
+  }
+
   void eval_complete_into(pc_density d, bool need_h, double* stats) override {
     if (kept_nc == 0) throw computation_error("no kept evaluation to complete");
     EvalStats tmp;
@@ -1352,30 +1402,12 @@ struct DeviceCtx : Evaluator {
     double* st = ensure(d_stats, cap_stats, total);
     const size_t e1 = (need_h ? 2 : 1) * nc * nc + nc;
     HIP_OK(hipEventRecord(ev[0], stream));
-#define PC_FROMY(NBV)                                                                             \
-  if (need_h) {                                                                                   \
-    switch (d.kind) {                                                                             \
-      case DENS_TANH: launch_fromy<NBV, true, DENS_TANH>(d.alpha, st); break;                    \
-      case DENS_EXP: launch_fromy<NBV, true, DENS_EXP>(d.alpha, st); break;                      \
-      default: launch_fromy<NBV, true, DENS_CUBE>(d.alpha, st); break;                           \
-    }                                                                                             \
-  } else {                                                                                        \
-    switch (d.kind) {                                                                             \
-      case DENS_TANH: launch_fromy<NBV, false, DENS_TANH>(d.alpha, st); break;                   \
-      case DENS_EXP: launch_fromy<NBV, false, DENS_EXP>(d.alpha, st); break;                     \
-      default: launch_fromy<NBV, false, DENS_CUBE>(d.alpha, st); break;                          \
-    }                                                                                             \
-  }
     switch (kept_nb) {
-      case 1: PC_FROMY(1); break;
-      case 2: PC_FROMY(2); break;
-      case 4: PC_FROMY(4); break;
-      default:
-        if (need_h) throw computation_error("split evaluation with H needs nc <= 64");
-        PC_FROMY(8);
-        break;
+      case 1: dispatch_fromy<1>(d, need_h, st); break;
+      case 2: dispatch_fromy<2>(d, need_h, st); break;
+      case 4: dispatch_fromy<4>(d, need_h, st); break;
+      default: dispatch_fromy<8>(d, need_h, st); break;
     }
-#undef PC_FROMY
     allreduce(st, e1);
     HIP_OK(hipMemcpyAsync(out->buf.data(), st, e1 * sizeof(double), hipMemcpyDeviceToHost, stream));
     finish_timing(true, 2);
