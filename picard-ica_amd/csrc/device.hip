@@ -284,15 +284,17 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     xrow_ok[p] = xk[p] < nf;
     xmu[p] = (xrow_ok[p] && mu) ? mu[xk[p]] : 0.0;
   }
-  double2 pre[PRE];
-  auto load_x = [&](uint64_t b) {  // b ≤ b_last: always a valid address
+  // two register sets for the X prefetch: the set stored in iteration b was
+  // loaded at the START of iteration b−1, a full iteration of latency hiding
+  double2 preA[PRE], preB[PRE];
+  auto load_x = [&](uint64_t b, double2 (&pre)[PRE]) {  // b ≤ b_last: always a valid address
 #pragma unroll
     for (int p = 0; p < PRE; ++p) {
       const int k = xrow_ok[p] ? xk[p] : 0;
       pre[p] = *reinterpret_cast<const double2*>(X + (size_t)k * ldx + b * TB + xt[p]);
     }
   };
-  auto store_x = [&](uint64_t b, double* xs) {
+  auto store_x = [&](uint64_t b, double* xs, const double2 (&pre)[PRE]) {
 #pragma unroll
     for (int p = 0; p < PRE; ++p) {
       const uint64_t tg = b * TB + xt[p];
@@ -365,24 +367,34 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 
   if (b_begin < b_end) {
     auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
-    // prologue: X(b0) → xs[0]; Y + density of b0 → img[0]; X(b0+1) → xs[1]
-    load_x(b_begin);
-    store_x(b_begin, xs0);
-    load_x(clampb(b_begin + 1));
+    // prologue: X(b0) → xs[0]; Y + density of b0 → img[0]; X(b0+1) → xs[1]; X(b0+2) → preA
+    load_x(b_begin, preA);
+    store_x(b_begin, xs0, preA);
+    load_x(clampb(b_begin + 1), preA);
     __syncthreads();
     elementwise(y_stage(xs0), b_begin, img0);
-    store_x(clampb(b_begin + 1), xs0 + XS);
-    load_x(clampb(b_begin + 2));
+    store_x(clampb(b_begin + 1), xs0 + XS, preA);
+    load_x(clampb(b_begin + 2), preA);
     __syncthreads();
-    int cur = 0;
-    for (uint64_t b = b_begin; b < b_last; ++b) {
+    // iteration b: Y stage of b+1 ‖ G stage of b; X(b+2) (loaded a full iteration
+    // ago) → xs[cur]; X(b+3) requested at the top
+    auto iter = [&](uint64_t b, int cur, double2 (&use)[PRE], double2 (&fill)[PRE]) {
+      load_x(clampb(b + 3), fill);
       const d4 yv = y_stage(xs0 + (cur ^ 1) * XS);     // block b+1
       g_stage(img0 + cur * NIMG * S::FRAGS);           // block b
       elementwise(yv, b + 1, img0 + (cur ^ 1) * NIMG * S::FRAGS);
-      store_x(clampb(b + 2), xs0 + cur * XS);
-      load_x(clampb(b + 3));
+      store_x(clampb(b + 2), xs0 + cur * XS, use);
       __syncthreads();
-      cur ^= 1;
+    };
+    uint64_t b = b_begin;
+    for (; b + 1 < b_last; b += 2) {
+      iter(b, 0, preA, preB);
+      iter(b + 1, 1, preB, preA);
+    }
+    int cur = 0;
+    if (b < b_last) {
+      iter(b, 0, preA, preB);
+      cur = 1;
     }
     g_stage(img0 + cur * NIMG * S::FRAGS);  // block b_last
     __syncthreads();
@@ -508,10 +520,12 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
   if (b_begin < b_end) {
     load_x(b_begin);
     store_x(b_begin, xs0);
-    load_x(clampb(b_begin + 1));
     __syncthreads();
     int cur = 0;
+    // iteration b: X(b+1) requested at the top, consumed (→ xs[cur^1]) after the
+    // Y stage and the density math of block b, which hide its latency
     for (uint64_t b = b_begin; b < b_end; ++b) {
+      load_x(clampb(b + 1));
       // four independent chains: no G stage here to hide the MFMA latency behind
       d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0}, yc = d4{0, 0, 0, 0}, yd = d4{0, 0, 0, 0};
       const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
@@ -528,8 +542,6 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
         for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
       }
       const d4 yv = (ya + yb) + (yc + yd);
-      store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
-      load_x(clampb(b + 2));
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const double y = yv[r];
@@ -538,6 +550,7 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
         rs_y2 = __builtin_fma(y, y, rs_y2);
         if constexpr (STORE) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = y;
       }
+      store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
       __syncthreads();
       cur ^= 1;
     }
