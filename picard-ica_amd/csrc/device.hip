@@ -722,6 +722,231 @@ __global__ void k_reduce_rows(const double* __restrict__ partials, int nwg, size
   out[e] = s;
 }
 
+// ---------------------------------------------------------------------------
+// Tiled two-phase pass for the shapes the register-resident fused kernel does
+// not cover: nc up to 256 (BASELINE C4: N = 256 non-ortho), nc ≤ 128 with H at
+// nc > 64, and any n_features (n_components < n_features).
+//   phase 1 (k_tiled_y): Y = W·(X−μ) per 128-sample tile as an LDS-tiled MFMA
+//     GEMM (W and X K-chunks of 32 staged in LDS), density, row sums, and
+//     y, ψ (, ψ′) written to HBM in MFMA-fragment order (512-B coalesced);
+//   phase 2 (k_tiled_gram): G_raw (, H_raw) = Σ_t ψ_t y_tᵀ (ψ′_t (y_t∘y_t)ᵀ) on
+//     MFMA, one 128×128 output tile per workgroup, T split over workgroups,
+//     fragments read straight from HBM into registers.
+// ---------------------------------------------------------------------------
+constexpr int TL_TT = 64;   // samples per phase-1 tile
+constexpr int TL_KC = 32;   // K chunk staged in LDS
+constexpr int TL_TS = TL_TT / 16;
+
+__host__ __device__ inline size_t tl_frag(uint64_t tt, int ib, int ts, int r, int nib) {
+  return ((((size_t)tt * nib + ib) * TL_TS + ts) * 4 + r) * 64;
+}
+
+template <int DENS, int MODE>  // MODE 0: full (write y, ψ, ψ′ + Σψ′, Σℓ, Σy²); 1: loss only (Σℓ, Σy²)
+__global__ void __launch_bounds__(FUSED_THREADS, 1)
+k_tiled_y(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int nfp, int ncp,
+          const double* __restrict__ WpT, const double* __restrict__ mu, double alpha, uint64_t tpw,
+          uint64_t n_tiles, double* __restrict__ partials, int accumulate, double* __restrict__ ybuf,
+          double* __restrict__ pbuf, double* __restrict__ dbuf) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  const int npair = ncp / 32;             // i-block pairs; wave w owns pair w (if w < npair)
+  const bool active = wave < npair;
+  const double inv_alpha = 1.0 / alpha;
+  constexpr int WSTR = 256 + 16;          // ws row stride (doubles): k-major, rows contiguous, padded
+  constexpr int XSTR = TL_TT + 16;        // xs row stride
+  extern __shared__ double smem[];
+  double* ws = smem;                      // [TL_KC][WSTR]
+  double* xs = ws + TL_KC * WSTR;         // [TL_KC][XSTR]
+  double* rsb = xs + TL_KC * XSTR;        // [3][256] row sums of the workgroup
+  for (int e = tid; e < 3 * 256; e += FUSED_THREADS) rsb[e] = 0.0;
+  double rs_d[2] = {0, 0}, rs_l[2] = {0, 0}, rs_y[2] = {0, 0};
+  const uint64_t t_begin = (uint64_t)blockIdx.x * tpw;
+  const uint64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
+  for (uint64_t tt = t_begin; tt < t_end; ++tt) {
+    d4 acc[2][TL_TS];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int t = 0; t < TL_TS; ++t) acc[i][t] = d4{0, 0, 0, 0};
+    for (int k0 = 0; k0 < nfp; k0 += TL_KC) {
+      __syncthreads();  // previous chunk fully consumed
+      // W chunk: ws[k][row] = Wᵀ[k0 + k][row] (host stores W transposed: coalesced both sides)
+      for (int e = tid; e < ncp * TL_KC; e += FUSED_THREADS) {
+        const int k = e / ncp, row = e % ncp;
+        ws[k * WSTR + row] = WpT[(size_t)(k0 + k) * ncp + row];
+      }
+      // X chunk: xs[k][t] = X[k0 + k][tile + t] − μ (zero outside)
+      for (int e = tid; e < TL_KC * TL_TT / 2; e += FUSED_THREADS) {
+        const int k = e / (TL_TT / 2), t = 2 * (e % (TL_TT / 2));
+        const int kg = k0 + k;
+        const uint64_t tg = tt * TL_TT + t;
+        double2 v = double2{0.0, 0.0};
+        if (kg < nf) {
+          const double2 xv = *reinterpret_cast<const double2*>(X + (size_t)kg * ldx + tg);
+          const double m = mu ? mu[kg] : 0.0;
+          v.x = tg < n_local ? xv.x - m : 0.0;
+          v.y = tg + 1 < n_local ? xv.y - m : 0.0;
+        }
+        *reinterpret_cast<double2*>(xs + k * XSTR + t) = v;
+      }
+      __syncthreads();
+      if (active) {
+#pragma unroll
+        for (int kq = 0; kq < TL_KC / 4; ++kq) {
+          double a[TL_TS], b[2];
+#pragma unroll
+          for (int t = 0; t < TL_TS; ++t) a[t] = xs[(kq * 4 + lk) * XSTR + t * 16 + lr];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) b[i] = ws[(kq * 4 + lk) * WSTR + (wave * 2 + i) * 16 + lr];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < TL_TS; ++t) acc[i][t] = mfma(a[t], b[i], acc[i][t]);
+        }
+      }
+    }
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ib = wave * 2 + i;
+#pragma unroll
+        for (int t = 0; t < TL_TS; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double y = acc[i][t][r];
+            const bool valid = tt * TL_TT + t * 16 + 4 * r + lk < n_local;
+            const size_t f = tl_frag(tt, ib, t, r, nib) + lane;
+            if constexpr (MODE == 0) {
+              double psi, dpsi, ll;
+              density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
+              rs_d[i] += valid ? dpsi : 0.0;
+              rs_l[i] += valid ? ll : 0.0;
+              ybuf[f] = y;
+              pbuf[f] = psi;
+              if (dbuf) dbuf[f] = valid ? dpsi : 0.0;
+            } else {
+              rs_l[i] += valid ? density_loss<DENS>(y, alpha, inv_alpha) : 0.0;
+            }
+            rs_y[i] = __builtin_fma(y, y, rs_y[i]);
+          }
+      }
+    }
+  }
+  // row sums → workgroup partials [Σψ′ | Σℓ | Σy²] (ncp each)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rs_d[i] += __shfl_xor(rs_d[i], 16); rs_d[i] += __shfl_xor(rs_d[i], 32);
+    rs_l[i] += __shfl_xor(rs_l[i], 16); rs_l[i] += __shfl_xor(rs_l[i], 32);
+    rs_y[i] += __shfl_xor(rs_y[i], 16); rs_y[i] += __shfl_xor(rs_y[i], 32);
+  }
+  __syncthreads();
+  if (active && lk == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wave * 2 + i) * 16 + lr;
+      rsb[row] = rs_d[i];
+      rsb[256 + row] = rs_l[i];
+      rsb[512 + row] = rs_y[i];
+    }
+  }
+  __syncthreads();
+  double* out = partials + (size_t)blockIdx.x * 3 * ncp;
+  for (int e = tid; e < 3 * ncp; e += FUSED_THREADS) {
+    const double v = rsb[(e / ncp) * 256 + e % ncp];
+    out[e] = accumulate ? out[e] + v : v;
+  }
+}
+
+// G_raw (, H_raw) tiles of 128×128 from the phase-1 fragments; blockIdx.x = tile, blockIdx.y = T split.
+template <bool NEED_H>
+__global__ void __launch_bounds__(FUSED_THREADS, 1)
+k_tiled_gram(const double* __restrict__ ybuf, const double* __restrict__ pbuf, const double* __restrict__ dbuf,
+             int ncp, uint64_t n_tiles, uint64_t tps, double* __restrict__ slabs, int accumulate) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  const int nto = (nib + 7) / 8;  // output tiles per dimension
+  const int ti = blockIdx.x / nto, tj = blockIdx.x % nto;
+  const int gi0 = ti * 8 + (wave >> 2) * 4, gj0 = tj * 8 + (wave & 3) * 2;
+  d4 accg[4][2], acch[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
+  bool iok[4], jok[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) iok[i] = gi0 + i < nib;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) jok[j] = gj0 + j < nib;
+  const uint64_t t_begin = (uint64_t)blockIdx.y * tps;
+  const uint64_t t_end = t_begin + tps < n_tiles ? t_begin + tps : n_tiles;
+  for (uint64_t tt = t_begin; tt < t_end; ++tt) {
+#pragma unroll 2
+    for (int t = 0; t < TL_TS; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double pa[4], da[4], yb[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const size_t f = tl_frag(tt, iok[i] ? gi0 + i : 0, t, r, nib) + lane;
+          pa[i] = iok[i] ? pbuf[f] : 0.0;
+          if constexpr (NEED_H) da[i] = iok[i] ? dbuf[f] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const size_t f = tl_frag(tt, jok[j] ? gj0 + j : 0, t, r, nib) + lane;
+          yb[j] = jok[j] ? ybuf[f] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            accg[i][j] = mfma(pa[i], yb[j], accg[i][j]);
+            if constexpr (NEED_H) acch[i][j] = mfma(da[i], yb[j] * yb[j], acch[i][j]);
+          }
+      }
+    }
+  }
+  const size_t nsq = (size_t)ncp * ncp;
+  double* slab = slabs + (size_t)blockIdx.y * (NEED_H ? 2 : 1) * nsq;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (iok[i] && jok[j])
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (gi0 + i) * 16 + lk + 4 * r, col = (gj0 + j) * 16 + lr;
+          const size_t o = (size_t)row * ncp + col;
+          slab[o] = accumulate ? slab[o] + accg[i][j][r] : accg[i][j][r];
+          if constexpr (NEED_H) slab[nsq + o] = accumulate ? slab[nsq + o] + acch[i][j][r] : acch[i][j][r];
+        }
+}
+
+// stats[e] for the tiled path: G/H from slabs (sum over splits), rows from phase-1 partials.
+__global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, const double* __restrict__ rows,
+                               int nwg1, int ncp, int nc, bool need_h, int rows_only, double* __restrict__ stats) {
+  const size_t nsq = (size_t)nc * nc, psq = (size_t)ncp * ncp;
+  const size_t mats = rows_only ? 0 : (need_h ? 2 : 1) * nsq;
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t base_rows = (need_h ? 2 : 1) * nsq;
+  if (e < mats) {
+    const size_t m = e / nsq, f = e % nsq;
+    const size_t src = m * psq + (f / nc) * ncp + f % nc;
+    double s = 0.0;
+    for (int k = 0; k < nsplit; ++k) s += slabs[(size_t)k * (need_h ? 2 : 1) * psq + src];
+    stats[e] = s;
+  } else if (e < mats + 3 * (size_t)nc) {
+    const size_t f = e - mats;
+    const size_t c = f / nc, row = f % nc;
+    if (rows_only && c == 0) return;  // loss-only: Σψ′ not computed
+    double s = 0.0;
+    for (int w = 0; w < nwg1; ++w) s += rows[(size_t)w * 3 * ncp + c * ncp + row];
+    stats[base_rows + f] = s;
+  }
+}
+
 // Fixed-order sum of per-workgroup partials into the compact stats layout
 // [G nc×nc | H nc×nc | Σψ′ nc | Σℓ nc | Σy² nc].
 __global__ void k_reduce(const double* __restrict__ partials, int nwg, size_t pstride, int ncp, int nc,
@@ -991,7 +1216,7 @@ struct DeviceCtx : Evaluator {
   ~DeviceCtx() override {
     (void)hipSetDevice(device);
     if (comm) ncclCommDestroy(comm);
-    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf})
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow})
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -1174,7 +1399,10 @@ struct DeviceCtx : Evaluator {
       dmu = ensure(d_mu, cap_mu, std::max<size_t>(nfp, nf));
       HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
     }
-    if (fused) {
+    const bool tiled = !fused && tiled_ok(nc, dens, alpha);
+    if (tiled) {
+      tiled_eval(w, nc, dmu, dens, alpha, need_h, st, 0);
+    } else if (fused) {
       const int ncp = 16 * nb;
       std::vector<double> wp((size_t)ncp * nfp, 0.0);
       for (size_t i = 0; i < nc; ++i)
@@ -1201,6 +1429,83 @@ struct DeviceCtx : Evaluator {
     last_call_ms = b;
     if (fused) { sum_kernel_ms += a; ++n_kernel; }
     sum_call_ms += b;
+  }
+
+  // ---- tiled two-phase path ----------------------------------------------
+  double* d_tbuf = nullptr; size_t cap_tbuf = 0;   // y, ψ, ψ′ fragments of one T chunk
+  double* d_slab = nullptr; size_t cap_slab = 0;
+  double* d_trow = nullptr; size_t cap_trow = 0;
+  static bool tiled_ok(size_t nc, int dens, double alpha) {
+    return nc <= 256 && !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0)) && dens <= DENS_LINEAR;
+  }
+  template <int D>
+  void tiled_launch(int mode, int nfp, int ncp, const double* dmu, double alpha, uint64_t tile0, uint64_t ntl,
+                    bool need_h, int nsplit, int nwg1, uint64_t tpw, bool acc, const double* X0) {
+    (void)tile0;
+    const size_t chunk = (size_t)ncp * ntl * TL_TT;
+    double* yb = d_tbuf;
+    double* pb = d_tbuf + chunk;
+    double* db = need_h ? d_tbuf + 2 * chunk : nullptr;
+    const size_t lds = (size_t)(TL_KC * (256 + 16) + TL_KC * (TL_TT + 16) + 3 * 256) * sizeof(double);
+    static bool attr[2] = {false, false};
+    auto k1 = mode == 0 ? k_tiled_y<D, 0> : k_tiled_y<D, 1>;
+    if (!attr[mode]) {
+      HIP_OK(hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr[mode] = true;
+    }
+    const uint64_t n_in_chunk = std::min<uint64_t>(n_local_ - tile0 * TL_TT, ntl * TL_TT);
+    k1<<<nwg1, FUSED_THREADS, lds, stream>>>(X0, ldx, n_in_chunk, (int)nf, nfp, ncp, d_w, dmu, alpha, tpw, ntl,
+                                             d_trow, acc ? 1 : 0, yb, pb, db);
+    HIP_OK(hipGetLastError());
+    if (mode == 0) {
+      const int nto = (ncp / 16 + 7) / 8;
+      const uint64_t tps = (ntl + nsplit - 1) / nsplit;
+      if (need_h)
+        k_tiled_gram<true><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      else
+        k_tiled_gram<false><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      HIP_OK(hipGetLastError());
+    }
+  }
+  // mode 0: all stats; mode 1: Σℓ, Σy² only (loss-only try; the completion recomputes)
+  void tiled_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st,
+                  int mode) {
+    const int ncp = (int)((nc + 31) / 32 * 32);
+    const int nfp = (int)((nf + TL_KC - 1) / TL_KC * TL_KC);
+    std::vector<double> wt((size_t)nfp * ncp, 0.0);  // Wᵀ, zero-padded
+    for (size_t i = 0; i < nc; ++i)
+      for (size_t k = 0; k < nf; ++k) wt[k * ncp + i] = w[i * nf + k];
+    ensure(d_w, cap_w, wt.size());
+    HIP_OK(hipMemcpyAsync(d_w, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    const uint64_t n_tiles = (n_local_ + TL_TT - 1) / TL_TT;
+    // T chunks bound the fragment buffers to ~24 GB (3 arrays of ncp × chunk)
+    const uint64_t max_tiles = std::max<uint64_t>(1, (uint64_t)(24e9 / (3.0 * ncp * TL_TT * sizeof(double))));
+    const uint64_t ct = std::min<uint64_t>(n_tiles, max_tiles);
+    const int nwg1 = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(ct, 1));
+    const int nto = (ncp / 16 + 7) / 8;
+    const int nsplit = (int)std::max<uint64_t>(1, std::min<uint64_t>(ct, (uint64_t)(2 * n_cu / (nto * nto))));
+    if (mode == 0) {
+      ensure(d_tbuf, cap_tbuf, (size_t)(need_h ? 3 : 2) * ncp * ct * TL_TT);
+      ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
+    }
+    ensure(d_trow, cap_trow, (size_t)nwg1 * 3 * ncp);
+    for (uint64_t t0 = 0; t0 < std::max<uint64_t>(n_tiles, 1); t0 += ct) {
+      const uint64_t ntl = std::min<uint64_t>(ct, n_tiles - t0);
+      const uint64_t tpw = (ntl + nwg1 - 1) / nwg1;
+      const bool acc = t0 > 0;
+      const double* X0 = X + t0 * TL_TT;
+      switch (dens) {
+        case DENS_TANH: tiled_launch<DENS_TANH>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
+        case DENS_EXP: tiled_launch<DENS_EXP>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
+        case DENS_CUBE: tiled_launch<DENS_CUBE>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
+        default: tiled_launch<DENS_LINEAR>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
+      }
+      if (n_tiles == 0) break;
+    }
+    const size_t total = (size_t)(mode == 0 ? (need_h ? 2 : 1) * nc * nc : 0) + 3 * nc;
+    k_reduce_tiled<<<(total + 255) / 256, 256, 0, stream>>>(d_slab, nsplit, d_trow, nwg1, ncp, (int)nc, need_h,
+                                                            mode == 1 ? 1 : 0, st);
+    HIP_OK(hipGetLastError());
   }
 
   void generic_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st) {
@@ -1328,9 +1633,38 @@ struct DeviceCtx : Evaluator {
 
   bool eval_loss(const double* w, size_t nc, const double* mu, pc_density d, bool need_h, EvalStats* out) override {
     if (!fused_ok(nc, d.kind, d.alpha, need_h)) {
-      eval(w, nc, mu, d, need_h, out);
-      return false;
+      if (!tiled_ok(nc, d.kind, d.alpha)) {
+        eval(w, nc, mu, d, need_h, out);
+        return false;
+      }
+      // tiled shapes: loss-only phase 1 now, full recompute (phase 1 + 2) on completion
+      HIP_OK(hipSetDevice(device));
+      out->nc = nc;
+      out->has_h = need_h;
+      out->buf.assign(EvalStats::size(nc, need_h), 0.0);
+      const size_t total = EvalStats::size(nc, need_h);
+      double* st = ensure(d_stats, cap_stats, total);
+      HIP_OK(hipEventRecord(ev[0], stream));
+      double* dmu = nullptr;
+      if (mu) {
+        dmu = ensure(d_mu, cap_mu, nf);
+        HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+      }
+      HIP_OK(hipEventRecord(ev[1], stream));
+      tiled_eval(w, nc, dmu, d.kind, d.alpha, need_h, st, 1);
+      HIP_OK(hipEventRecord(ev[2], stream));
+      allreduce(st + total - 2 * nc, 2 * nc);
+      HIP_OK(hipMemcpyAsync(out->buf.data() + total - 2 * nc, st + total - 2 * nc, 2 * nc * sizeof(double),
+                            hipMemcpyDeviceToHost, stream));
+      finish_timing(true, 1);
+      kept_tiled = true;
+      kept_nc = nc;
+      kept_w.assign(w, w + nc * nf);
+      kept_mu.assign(mu ? mu : w, mu ? mu + nf : w);
+      kept_has_mu = mu != nullptr;
+      return true;
     }
+    kept_tiled = false;
     HIP_OK(hipSetDevice(device));
     const int nb = pick_nb(nc);
     const int nfp = 16 * nb;
@@ -1408,8 +1742,20 @@ struct DeviceCtx : Evaluator {
     std::memcpy(stats, tmp.buf.data(), e1 * sizeof(double));
   }
 
+  bool kept_tiled = false, kept_has_mu = false;
+  std::vector<double> kept_w, kept_mu;
+
   void eval_complete(pc_density d, bool need_h, EvalStats* out) override {
     HIP_OK(hipSetDevice(device));
+    if (kept_tiled) {  // recompute phase 1 in full mode + phase 2 at the kept W
+      const size_t nc = kept_nc;
+      const size_t total = EvalStats::size(nc, need_h);
+      std::vector<double> full(total);
+      run_eval(kept_w.data(), nc, kept_has_mu ? kept_mu.data() : nullptr, d.kind, d.alpha, need_h, full.data());
+      const size_t e1 = (need_h ? 2 : 1) * nc * nc + nc;
+      std::memcpy(out->buf.data(), full.data(), e1 * sizeof(double));
+      return;
+    }
     const size_t nc = kept_nc;
     const size_t total = EvalStats::size(nc, need_h);
     double* st = ensure(d_stats, cap_stats, total);

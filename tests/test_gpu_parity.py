@@ -37,7 +37,7 @@ def ctx_with(pa, x):
 DENSITIES = [("tanh", 1.0), ("tanh", 0.7), ("exp", 1.0), ("exp", 0.1), ("cube", 1.0)]
 
 
-@pytest.mark.parametrize("n", [8, 16, 30, 64, 100, 128, 160])
+@pytest.mark.parametrize("n", [8, 16, 30, 64, 100, 128, 160, 256])
 @pytest.mark.parametrize("dens", DENSITIES)
 @pytest.mark.parametrize("need_h", [False, True])
 def test_eval_stats_vs_oracle(pa, po, rng, n, dens, need_h):
@@ -77,7 +77,7 @@ def test_eval_no_mean_and_tiny_t(pa, po, rng):
             assert rel_err(got[k], want[k]) <= TOL, (t, k)
 
 
-@pytest.mark.parametrize("n", [8, 30, 64, 128])
+@pytest.mark.parametrize("n", [8, 30, 64, 128, 200])
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
 @pytest.mark.parametrize("need_h", [False, True])
 def test_split_eval_bit_identical(pa, rng, n, dens, need_h):
@@ -196,6 +196,26 @@ def test_jade_long_run_properties(pa, c1_data):
     assert r.converged
     w = r.unmixing
     assert np.max(np.abs(w @ w.T - np.eye(8))) < 1e-6
+
+
+def test_c4_shape_nonortho_vs_oracle(pa, po, dg):
+    """BASELINE config 4's shape (N = 256, non-ortho, m = 7) at a T the oracle runs in
+    seconds: the tiled MFMA path end to end, first iterations against the oracle."""
+    x, s, a = dg.generate_data(256, 20000, 42)
+    kw = dict(ortho=False, extended=False, m=7, max_iter=6)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    sv = pa.Solver(ctx, pa.PicardConfig(w_init=np.eye(256), **kw))
+    losses = []
+    done = False
+    while not done:
+        done = sv.step()
+        losses.append(sv.last()[0])
+    r = sv.finish()
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(256), **kw))
+    assert r.n_iterations == ro.n_iterations == 6
+    assert np.allclose(losses, ro.info.trace_loss, rtol=1e-10, atol=0)
+    assert np.max(np.abs(r.unmixing - ro.unmixing)) <= 1e-8
 
 
 def test_transform_and_mixing(pa, po, c1_data):

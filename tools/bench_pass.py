@@ -23,7 +23,7 @@ for _ in range(reps):
     ctx.eval(w, mu, d, need_h)
 wall = (time.perf_counter() - t0) / reps
 k, c, nl = ctx.kernel_stats()
-avg = k / max(nl, 1)
+avg = k / nl if nl else c / max(reps, 1)  # tiled / generic paths: whole eval call
 fl = (6.0 if need_h else 4.0) * n * n * t
 print(f"N={n} T={t} {dens} H={need_h}: kernel {avg:.3f} ms  call {c/max(nl,1):.3f} ms  wall {wall*1e3:.3f} ms  "
       f"{fl/avg/1e9:.2f} TF/s ({fl/avg/1e9/78.6*100:.1f}% of 78.6)  HBM {8*n*t/avg/1e6:.1f} GB/s", flush=True)
