@@ -1631,7 +1631,8 @@ struct DeviceCtx : Evaluator {
   double sum_split_ms = 0;
   uint64_t n_split = 0;
 
-  bool eval_loss(const double* w, size_t nc, const double* mu, pc_density d, bool need_h, EvalStats* out) override {
+  bool eval_loss(const double* w, size_t nc, const double* mu, pc_density d, bool need_h, EvalStats* out,
+                 bool keep = true) override {
     if (!fused_ok(nc, d.kind, d.alpha, need_h)) {
       if (!tiled_ok(nc, d.kind, d.alpha)) {
         eval(w, nc, mu, d, need_h, out);
@@ -1668,11 +1669,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     const int nb = pick_nb(nc);
     const int nfp = 16 * nb;
-    const bool store = ensure_ybuf(nb);
-    if (!store) {  // no room to keep Y: a complete pass instead
-      eval(w, nc, mu, d, need_h, out);
-      return false;
-    }
+    // keep == false, or no room for Y: loss-only pass, completion recomputes the full pass
+    const bool store = keep && ensure_ybuf(nb);
     out->nc = nc;
     out->has_h = need_h;
     out->buf.assign(EvalStats::size(nc, need_h), 0.0);
@@ -1710,6 +1708,12 @@ struct DeviceCtx : Evaluator {
     finish_timing(true, 1);
     kept_nc = nc;
     kept_nb = nb;
+    kept_tiled = !store;  // "recompute" completion
+    if (!store) {
+      kept_w.assign(w, w + nc * nf);
+      kept_mu.assign(mu ? mu : w, mu ? mu + nf : w);
+      kept_has_mu = mu != nullptr;
+    }
     return true;
   }
 

@@ -58,11 +58,13 @@ class Evaluator {
   virtual uint64_t n_local() const = 0;
   virtual void moments4(const double* w, size_t nc, const double* mu, double* out) = 0;
   // Line-search try (core.rs:124-127 only needs Σℓ, Σy²). May compute just
-  // those and keep Y on the device; returns true in that case, and then
-  // eval_complete fills G (H) and Σψ′ of the SAME W from the kept Y. A
-  // device that cannot split falls back to a full pass and returns false.
+  // those; returns true in that case, and then eval_complete fills G (H) and
+  // Σψ′ of the SAME W — from Y kept in HBM when `keep` and there is room,
+  // otherwise by recomputing the pass. A device that cannot split falls back
+  // to a full pass and returns false.
   virtual bool eval_loss(const double* w, size_t nc, const double* mu, pc_density d, bool need_h,
-                         EvalStats* out) {
+                         EvalStats* out, bool keep = true) {
+    (void)keep;
     eval(w, nc, mu, d, need_h, out);
     return false;
   }

@@ -207,6 +207,8 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
     std::fflush(stdout);
   }
   trace_ = std::getenv("PICARD_TRACE") != nullptr;
+  keep_y_ = std::getenv("PICARD_KEEP_Y") != nullptr;
+  split_first_ = std::getenv("PICARD_SPLIT_FIRST") != nullptr;
   init_core();
 }
 
@@ -219,7 +221,8 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
 
 bool Solver::evaluate_loss(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
-  const bool partial = ev_->eval_loss(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
+  const bool partial =
+      ev_->eval_loss(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out, keep_y_);
   ++last_evals_;
   ++total_evals_;
   return partial;
@@ -297,7 +300,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries) {  // c
       for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += alpha * direction.a[e];
     }
     r.w = matmul(transform, W_);
-    if (k == 0 && first_full_) {
+    if (k == 0 && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
     } else {

@@ -76,9 +76,17 @@ class Solver {
   bool converged_ = false, done_ = false;
   uint64_t last_evals_ = 0, total_evals_ = 0;
   uint64_t total_completions_ = 0;
-  // first try of a line search as a full fused pass while first tries keep
-  // being accepted; otherwise loss-only tries + one completion pass
+  // Evaluation schedule of a line search (results are bit-identical whatever
+  // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
+  // the bench data, and then its G is the next gradient); tries ≥ 2 are
+  // loss-only passes (about 0.6 of a fused pass) and only the accepted one is
+  // completed, by recomputing it in full. Knobs for experiments:
+  //   PICARD_KEEP_Y=1      loss-only tries keep Y in HBM (completion ≈ 0.5 pass,
+  //                        each try pays the Y write ≈ 0.1 pass)
+  //   PICARD_SPLIT_FIRST=1 try 1 is loss-only too unless the last line search
+  //                        accepted at try 1
   bool first_full_ = true;
+  bool keep_y_ = false, split_first_ = false;
   bool trace_ = false;  // PICARD_TRACE=1: one stderr line per iteration (line-search tries)
 };
 
