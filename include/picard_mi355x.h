@@ -159,6 +159,16 @@ int pc_ctx_eval(pc_ctx* ctx, const double* w /* nc × n_features */, uint64_t nc
  * pc_ctx_eval's. */
 int pc_ctx_eval_loss(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, pc_density density,
                      uint32_t flags, double* stats, int32_t* kept, char* err, size_t errlen);
+/* Non-orthogonal line search in one pass (core.rs:117-140 with the try
+ * transform M = I + α·D, solver.rs's non-ortho branch): with w = W·P and
+ * z = (D·W)·P (both nc × n_features), writes Σℓ and Σy² of
+ * Y_j = (w + α_j·z)·(X − μ) for every α_j: ll_out[j·nc + i], y2_out[j·nc + i].
+ * Equal to pc_ctx_eval_loss at w + α_j·z up to rounding (Y_j is formed as
+ * Y + α_j·Z). Returns PC_ERR_COMPUTATION for a shape the pass does not cover
+ * (nc > 256, or a negative tanh/exp α). */
+int pc_ctx_eval_loss_multi(pc_ctx* ctx, const double* w, const double* z, uint64_t nc, const double* mu,
+                           pc_density density, const double* alphas, uint64_t n_alpha, double* ll_out,
+                           double* y2_out, char* err, size_t errlen);
 int pc_ctx_eval_complete(pc_ctx* ctx, pc_density density, uint32_t flags, double* stats, char* err,
                          size_t errlen);
 int pc_ctx_rowsum(pc_ctx* ctx, double* out /* n_features */, char* err, size_t errlen);
@@ -213,7 +223,7 @@ void pc_ctx_kernel_stats(pc_ctx* ctx, double* kernel_ms, double* call_ms, uint64
                          int32_t reset);
 /* Per kernel kind since the last reset: [0] fused pass, [1] loss-only try,
  * [2] completion from kept Y — summed HIP-event kernel ms and launch counts. */
-void pc_ctx_kernel_breakdown(pc_ctx* ctx, double ms[3], uint64_t n[3], int32_t reset);
+void pc_ctx_kernel_breakdown(pc_ctx* ctx, double ms[4], uint64_t n[4], int32_t reset);
 /* hipDeviceSynchronize on `device` (bench bracketing). */
 int pc_device_synchronize(int32_t device);
 

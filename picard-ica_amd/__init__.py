@@ -159,6 +159,7 @@ def _load():
         "pc_ctx_t0": (u64, [vp]),
         "pc_ctx_eval": (C.c_int, [vp, d, u64, d, _Density, C.c_uint32, d, cp, sz]),
         "pc_ctx_eval_loss": (C.c_int, [vp, d, u64, d, _Density, C.c_uint32, d, P(i32), cp, sz]),
+        "pc_ctx_eval_loss_multi": (C.c_int, [vp, d, d, u64, d, _Density, d, u64, d, d, cp, sz]),
         "pc_ctx_eval_complete": (C.c_int, [vp, _Density, C.c_uint32, d, cp, sz]),
         "pc_ctx_rowsum": (C.c_int, [vp, d, cp, sz]),
         "pc_ctx_gram": (C.c_int, [vp, d, d, cp, sz]),
@@ -190,7 +191,7 @@ EXPORTED = [
     "pc_full_unmixing", "pc_mixing", "pc_result_free", "pc_amari_distance", "pc_permute",
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
-    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
+    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
     "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
@@ -559,6 +560,19 @@ class DeviceContext:
             _raise(lib.pc_ctx_eval_complete(self.h, density._c(), 1 if need_h else 0, _ptr(st), err, len(err)), err)
         return self._unpack(loss_only, nc, need_h), bool(kept.value), self._unpack(st, nc, need_h)
 
+    def eval_loss_multi(self, w, z, alphas, mu=None, density: DensityType = DensityType()):
+        """pc_ctx_eval_loss_multi: (Σℓ, Σy²) of (w + α_j·z)(X − μ) for every α_j, each [n_alpha, nc]."""
+        w, z = _c64(w), _c64(z)
+        nc = w.shape[0]
+        al = _c64(np.asarray(alphas, dtype=np.float64).ravel())
+        mu_a = _c64(mu) if mu is not None else None
+        ll = np.empty((len(al), nc))
+        y2 = np.empty((len(al), nc))
+        err = _errbuf()
+        _raise(lib.pc_ctx_eval_loss_multi(self.h, _ptr(w), _ptr(z), nc, _ptr(mu_a) if mu_a is not None else None,
+                                          density._c(), _ptr(al), len(al), _ptr(ll), _ptr(y2), err, len(err)), err)
+        return ll, y2
+
     def last_timing(self):
         k, c = C.c_double(), C.c_double()
         lib.pc_ctx_last_timing(self.h, C.byref(k), C.byref(c))
@@ -571,11 +585,11 @@ class DeviceContext:
         return k.value, c.value, n.value
 
     def kernel_breakdown(self, reset: bool = False) -> dict:
-        """{kind: (Σ kernel ms, launches)} for kind in fused / loss / fromy (HIP events)."""
-        ms = (C.c_double * 3)()
-        n = (C.c_uint64 * 3)()
+        """{kind: (Σ kernel ms, launches)} for kind in fused / loss / fromy / multi (HIP events)."""
+        ms = (C.c_double * 4)()
+        n = (C.c_uint64 * 4)()
         lib.pc_ctx_kernel_breakdown(self.h, ms, n, int(reset))
-        return {k: (ms[i], n[i]) for i, k in enumerate(("fused", "loss", "fromy"))}
+        return {k: (ms[i], n[i]) for i, k in enumerate(("fused", "loss", "fromy", "multi"))}
 
     def rowsum(self) -> np.ndarray:
         out = np.empty(self.n_features)

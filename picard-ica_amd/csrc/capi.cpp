@@ -322,6 +322,18 @@ int pc_ctx_eval_loss(pc_ctx* c, const double* w, uint64_t nc, const double* mu, 
   });
 }
 
+int pc_ctx_eval_loss_multi(pc_ctx* c, const double* w, const double* z, uint64_t nc, const double* mu,
+                           pc_density d, const double* alphas, uint64_t n_alpha, double* ll_out, double* y2_out,
+                           char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
+    if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
+    if (n_alpha == 0) return;
+    if (!c->ev->eval_loss_multi(w, z, nc, mu, d, alphas, (int)n_alpha, ll_out, y2_out))
+      throw computation_error("multi-try loss pass not available for this shape");
+  });
+}
+
 int pc_ctx_eval_complete(pc_ctx* c, pc_density d, uint32_t flags, double* stats, char* err, size_t errlen) {
   return guarded(err, errlen, [&] {
     // only the entries [G | H | Σψ′] are written; Σℓ, Σy² of `stats` are left as they are
@@ -353,7 +365,7 @@ void pc_ctx_kernel_stats(pc_ctx* c, double* kernel_ms, double* call_ms, uint64_t
   device_ctx_kernel_stats(c->ev.get(), kernel_ms, call_ms, n, reset);
 }
 
-void pc_ctx_kernel_breakdown(pc_ctx* c, double ms[3], uint64_t n[3], int32_t reset) {
+void pc_ctx_kernel_breakdown(pc_ctx* c, double ms[4], uint64_t n[4], int32_t reset) {
   device_ctx_kernel_breakdown(c->ev.get(), ms, n, reset);
 }
 

@@ -78,17 +78,17 @@ __device__ __forceinline__ void exp_parts(double x, double& em_r, double& scale)
   scale = __builtin_ldexp(1.0, (int)kf);
 }
 
-__device__ __forceinline__ double rcp_nr(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  double e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
-  return __builtin_fma(r, e, r);
+// v_rcp_f64 is good to ~2^-25 (tools/microbench/rcp_acc.hip: 2.4e8 ulp raw,
+// 9.9 ulp after one Newton step, 0.5 ulp after two)
+__device__ __forceinline__ double rcp_nr1(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
 }
 
-// n / d with one residual correction (≤ 1 ulp)
+// n / d: one Newton step on the reciprocal, then one residual correction of
+// the quotient (error ≈ ε_r² + rounding: ≤ 1 ulp) — 6 fp64 ops
 __device__ __forceinline__ double div_nr(double n, double d) {
-  const double r = rcp_nr(d);
+  const double r = rcp_nr1(d);
   const double q = n * r;
   return __builtin_fma(__builtin_fma(-d, q, n), r, q);
 }
@@ -924,6 +924,132 @@ k_tiled_gram(const double* __restrict__ ybuf, const double* __restrict__ pbuf, c
         }
 }
 
+// ---------------------------------------------------------------------------
+// Non-orthogonal line search in ONE pass (core.rs:117-140 with M = I + αD):
+// Y_α = (W + α·DW)·(X−μ) = Y + α·Z, so Y = W·(X−μ) and Z = (DW)·(X−μ) are
+// computed once (two MFMA GEMMs) and Σℓ(Y_α), Σ(Y_α)² are accumulated for
+// every remaining try α_j (VALU only). The host then walks the tries in the
+// reference's order and stops at the first accepted α exactly as
+// line_search does; only the accepted try is then evaluated in full.
+// ---------------------------------------------------------------------------
+constexpr int ML_NA = 12;   // tries per pass (ls_tries − 1 ≤ 12; more are chunked)
+constexpr int ML_KC = 16;   // K chunk (two W images in LDS)
+constexpr int ML_TS = 2, ML_TT = 16 * ML_TS;  // samples per tile (Y and Z accumulators in VGPRs)
+
+template <int DENS>
+__global__ void __launch_bounds__(FUSED_THREADS, 1)
+k_multi_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int nfp, int ncp,
+             const double* __restrict__ WpT, const double* __restrict__ ZpT, const double* __restrict__ mu,
+             double alpha, const double* __restrict__ alphas, int na, uint64_t tpw, uint64_t n_tiles,
+             double* __restrict__ partials) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int npair = ncp / 32;
+  const bool active = wave < npair;
+  const double inv_alpha = 1.0 / alpha;
+  constexpr int WSTR = 256 + 16, XSTR = ML_TT + 16;
+  extern __shared__ double smem[];
+  double* ws = smem;                  // [ML_KC][WSTR]
+  double* zs = ws + ML_KC * WSTR;     // [ML_KC][WSTR]
+  double* xs = zs + ML_KC * WSTR;     // [ML_KC][XSTR]
+  // per-try row sums live in LDS, one region per wave: rs[wave][j][i][lr][Σℓ, Σy²]
+  double* rs = xs + ML_KC * XSTR + (size_t)wave * ML_NA * 2 * 16 * 2;
+  for (int e = lane; e < ML_NA * 2 * 16 * 2; e += 64) rs[e] = 0.0;
+  const uint64_t t_begin = (uint64_t)blockIdx.x * tpw;
+  const uint64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
+  for (uint64_t tt = t_begin; tt < t_end; ++tt) {
+    d4 ay[2][ML_TS], az[2][ML_TS];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int t = 0; t < ML_TS; ++t) { ay[i][t] = d4{0, 0, 0, 0}; az[i][t] = d4{0, 0, 0, 0}; }
+    for (int k0 = 0; k0 < nfp; k0 += ML_KC) {
+      __syncthreads();
+      for (int e = tid; e < ncp * ML_KC; e += FUSED_THREADS) {
+        const int k = e / ncp, row = e % ncp;
+        ws[k * WSTR + row] = WpT[(size_t)(k0 + k) * ncp + row];
+        zs[k * WSTR + row] = ZpT[(size_t)(k0 + k) * ncp + row];
+      }
+      for (int e = tid; e < ML_KC * ML_TT / 2; e += FUSED_THREADS) {
+        const int k = e / (ML_TT / 2), t = 2 * (e % (ML_TT / 2));
+        const int kg = k0 + k;
+        const uint64_t tg = tt * ML_TT + t;
+        double2 v = double2{0.0, 0.0};
+        if (kg < nf) {
+          const double2 xv = *reinterpret_cast<const double2*>(X + (size_t)kg * ldx + tg);
+          const double m = mu ? mu[kg] : 0.0;
+          v.x = tg < n_local ? xv.x - m : 0.0;
+          v.y = tg + 1 < n_local ? xv.y - m : 0.0;
+        }
+        *reinterpret_cast<double2*>(xs + k * XSTR + t) = v;
+      }
+      __syncthreads();
+      if (active) {
+#pragma unroll
+        for (int kq = 0; kq < ML_KC / 4; ++kq) {
+          double a[ML_TS], bw[2], bz[2];
+#pragma unroll
+          for (int t = 0; t < ML_TS; ++t) a[t] = xs[(kq * 4 + lk) * XSTR + t * 16 + lr];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            bw[i] = ws[(kq * 4 + lk) * WSTR + (wave * 2 + i) * 16 + lr];
+            bz[i] = zs[(kq * 4 + lk) * WSTR + (wave * 2 + i) * 16 + lr];
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < ML_TS; ++t) {
+              ay[i][t] = mfma(a[t], bw[i], ay[i][t]);
+              az[i][t] = mfma(a[t], bz[i], az[i][t]);
+            }
+        }
+      }
+    }
+    if (active) {
+#pragma unroll 1
+      for (int j = 0; j < na; ++j) {
+        const double aj = alphas[j];  // uniform: scalar load
+        double sl[2] = {0.0, 0.0}, sq[2] = {0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int t = 0; t < ML_TS; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const bool valid = tt * ML_TT + t * 16 + 4 * r + lk < n_local;
+              const double y = __builtin_fma(aj, az[i][t][r], ay[i][t][r]);
+              sl[i] += valid ? density_loss<DENS>(y, alpha, inv_alpha) : 0.0;
+              sq[i] = __builtin_fma(y, y, sq[i]);
+              if (r == 3) __builtin_amdgcn_sched_barrier(0);  // 4 density chains live at a time
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          double l = sl[i], q = sq[i];
+          l += __shfl_xor(l, 16); l += __shfl_xor(l, 32);
+          q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+          if (lk == 0) {
+            double* p = rs + ((j * 2 + i) * 16 + lr) * 2;
+            p[0] += l;
+            p[1] += q;
+          }
+        }
+      }
+    }
+  }
+  // partials: [na][2][ncp] (Σℓ, Σy² per try)
+  double* out = partials + (size_t)blockIdx.x * ML_NA * 2 * ncp;
+  if (active && lk == 0)
+    for (int j = 0; j < na; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wave * 2 + i) * 16 + lr;
+        const double* p = rs + ((j * 2 + i) * 16 + lr) * 2;
+        out[(j * 2 + 0) * ncp + row] = p[0];
+        out[(j * 2 + 1) * ncp + row] = p[1];
+      }
+}
+
+
 // stats[e] for the tiled path: G/H from slabs (sum over splits), rows from phase-1 partials.
 __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, const double* __restrict__ rows,
                                int nwg1, int ncp, int nc, bool need_h, int rows_only, double* __restrict__ stats) {
@@ -1401,7 +1527,9 @@ struct DeviceCtx : Evaluator {
     }
     const bool tiled = !fused && tiled_ok(nc, dens, alpha);
     if (tiled) {
+      HIP_OK(hipEventRecord(ev[1], stream));
       tiled_eval(w, nc, dmu, dens, alpha, need_h, st, 0);
+      HIP_OK(hipEventRecord(ev[2], stream));
     } else if (fused) {
       const int ncp = 16 * nb;
       std::vector<double> wp((size_t)ncp * nfp, 0.0);
@@ -1423,12 +1551,78 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventRecord(ev[3], stream));
     HIP_OK(hipStreamSynchronize(stream));
     float a = 0, b = 0;
-    if (fused) { HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2])); }
+    const bool timed = fused || tiled;  // "fused" kind = every full pass (fused or tiled)
+    if (timed) { HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2])); }
     HIP_OK(hipEventElapsedTime(&b, ev[0], ev[3]));
-    last_kernel_ms = fused ? a : b;
+    last_kernel_ms = timed ? a : b;
     last_call_ms = b;
-    if (fused) { sum_kernel_ms += a; ++n_kernel; }
+    if (timed) { sum_kernel_ms += a; ++n_kernel; }
     sum_call_ms += b;
+  }
+
+  // ---- non-ortho multi-try loss pass ---------------------------------------
+  // ll_out / y2_out: [na][nc] (Σℓ, Σy² of Y + α_j·Z), summed over ranks
+  void multi_loss(const double* w, const double* z, size_t nc, const double* mu, pc_density d, const double* alphas,
+                  int na, double* ll_out, double* y2_out) {
+    HIP_OK(hipSetDevice(device));
+    const int ncp = (int)((nc + 31) / 32 * 32);
+    const int nfp = (int)((nf + ML_KC - 1) / ML_KC * ML_KC);
+    std::vector<double> wt((size_t)2 * nfp * ncp + ML_NA, 0.0);
+    for (size_t i = 0; i < nc; ++i)
+      for (size_t k = 0; k < nf; ++k) {
+        wt[k * ncp + i] = w[i * nf + k];
+        wt[(size_t)nfp * ncp + k * ncp + i] = z[i * nf + k];
+      }
+    for (int j = 0; j < na; ++j) wt[(size_t)2 * nfp * ncp + j] = alphas[j];
+    double* dw = ensure(d_w, cap_w, wt.size());
+    HIP_OK(hipEventRecord(ev[0], stream));
+    HIP_OK(hipMemcpyAsync(dw, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    double* dmu = nullptr;
+    if (mu) {
+      dmu = ensure(d_mu, cap_mu, nf);
+      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    }
+    const uint64_t n_tiles = (n_local_ + ML_TT - 1) / ML_TT;
+    const int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_tiles, 1));
+    const uint64_t tpw = (std::max<uint64_t>(n_tiles, 1) + nwg - 1) / nwg;
+    const size_t pst = (size_t)ML_NA * 2 * ncp;
+    double* part = ensure(d_part, cap_part, (size_t)nwg * pst);
+    HIP_OK(hipMemsetAsync(part, 0, (size_t)nwg * pst * sizeof(double), stream));
+    const size_t lds = (size_t)(2 * ML_KC * (256 + 16) + ML_KC * (ML_TT + 16) + 8 * ML_NA * 2 * 16 * 2) * sizeof(double);
+    const double* dal = dw + (size_t)2 * nfp * ncp;
+    HIP_OK(hipEventRecord(ev[1], stream));
+    switch (d.kind) {
+      case DENS_TANH: k_multi_loss<DENS_TANH><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, nfp, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, tpw, n_tiles, part); break;
+      case DENS_EXP: k_multi_loss<DENS_EXP><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, nfp, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, tpw, n_tiles, part); break;
+      default: k_multi_loss<DENS_CUBE><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, nfp, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, tpw, n_tiles, part); break;
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    double* st = ensure(d_stats, cap_stats, (size_t)2 * na * nc);
+    // st[(j·2 + c)·nc + row] = Σ_w part[w][(j·2 + c)·ncp + row]
+    k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st);
+    HIP_OK(hipGetLastError());
+    allreduce(st, (size_t)2 * na * nc);
+    std::vector<double> h((size_t)2 * na * nc);
+    HIP_OK(hipMemcpyAsync(h.data(), st, h.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
+    finish_timing(true, 3);
+    for (int j = 0; j < na; ++j) {
+      std::memcpy(ll_out + (size_t)j * nc, h.data() + (size_t)(j * 2 + 0) * nc, nc * sizeof(double));
+      std::memcpy(y2_out + (size_t)j * nc, h.data() + (size_t)(j * 2 + 1) * nc, nc * sizeof(double));
+    }
+  }
+  bool multi_loss_ok(size_t nc, pc_density d) const {
+    return nc <= 256 && (d.kind == DENS_TANH || d.kind == DENS_EXP || d.kind == DENS_CUBE) &&
+           (d.kind == DENS_CUBE || d.alpha > 0.0) && std::getenv("PICARD_NO_MULTI") == nullptr;
+  }
+  bool eval_loss_multi(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
+                       const double* alphas, int na, double* ll_out, double* y2_out) override {
+    if (!multi_loss_ok(nc, d)) return false;
+    for (int j0 = 0; j0 < na; j0 += ML_NA) {
+      const int nj = std::min(ML_NA, na - j0);
+      multi_loss(w, z, nc, mu, d, alphas + j0, nj, ll_out + (size_t)j0 * nc, y2_out + (size_t)j0 * nc);
+    }
+    return true;
   }
 
   // ---- tiled two-phase path ----------------------------------------------
@@ -1613,7 +1807,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
   }
 
-  double sum_loss_ms = 0, sum_fromy_ms = 0;
+  double sum_loss_ms = 0, sum_fromy_ms = 0, sum_multi_ms = 0;
+  uint64_t n_multi = 0;
   uint64_t n_loss = 0, n_fromy = 0;
   void finish_timing(bool kernel_timed, int kind = 0) {
     HIP_OK(hipEventRecord(ev[3], stream));
@@ -1627,6 +1822,7 @@ struct DeviceCtx : Evaluator {
     if (kernel_timed) { sum_split_ms += a; ++n_split; }
     if (kind == 1) { sum_loss_ms += a; ++n_loss; }
     if (kind == 2) { sum_fromy_ms += a; ++n_fromy; }
+    if (kind == 3) { sum_multi_ms += a; ++n_multi; }
   }
   double sum_split_ms = 0;
   uint64_t n_split = 0;
@@ -1868,9 +2064,10 @@ void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int rese
   ms[0] = d->sum_kernel_ms; n[0] = d->n_kernel;
   ms[1] = d->sum_loss_ms; n[1] = d->n_loss;
   ms[2] = d->sum_fromy_ms; n[2] = d->n_fromy;
+  ms[3] = d->sum_multi_ms; n[3] = d->n_multi;
   if (reset) {
-    d->sum_kernel_ms = d->sum_loss_ms = d->sum_fromy_ms = d->sum_split_ms = d->sum_call_ms = 0;
-    d->n_kernel = d->n_loss = d->n_fromy = d->n_split = 0;
+    d->sum_kernel_ms = d->sum_loss_ms = d->sum_fromy_ms = d->sum_split_ms = d->sum_call_ms = d->sum_multi_ms = 0;
+    d->n_kernel = d->n_loss = d->n_fromy = d->n_split = d->n_multi = 0;
   }
 }
 void device_synchronize(int device) {

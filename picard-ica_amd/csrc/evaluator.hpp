@@ -69,6 +69,13 @@ class Evaluator {
     return false;
   }
   virtual void eval_complete(pc_density d, bool need_h, EvalStats* out) { (void)d; (void)need_h; (void)out; }
+  // Non-ortho line search: Σℓ and Σy² of Y_j = (W + α_j·Z)·(X−μ) for every α_j
+  // in one pass (ll_out, y2_out: [na][nc]). false = not supported here.
+  virtual bool eval_loss_multi(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
+                               const double* alphas, int na, double* ll_out, double* y2_out) {
+    (void)w; (void)z; (void)nc; (void)mu; (void)d; (void)alphas; (void)na; (void)ll_out; (void)y2_out;
+    return false;
+  }
   // eval_complete into a raw packed stats buffer (C ABI)
   virtual void eval_complete_into(pc_density d, bool need_h, double* stats) {
     (void)d; (void)need_h; (void)stats;

@@ -208,6 +208,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   }
   trace_ = std::getenv("PICARD_TRACE") != nullptr;
   keep_y_ = std::getenv("PICARD_KEEP_Y") != nullptr;
+  no_multi_ = std::getenv("PICARD_NO_MULTI") != nullptr;
   split_first_ = std::getenv("PICARD_SPLIT_FIRST") != nullptr;
   init_core();
 }
@@ -283,14 +284,16 @@ void Solver::init_core() {  // core.rs:175-209
   }
 }
 
-Solver::LsResult Solver::line_search(const Mat& direction, size_t tries) {  // core.rs:99-150
-  // Evaluation schedule (results are bit-identical either way): a try is a
-  // full fused pass, or a loss-only pass whose Y stays on the device and is
-  // completed (G, H, Σψ′) only if that try becomes the new iterate.
+Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first) {  // core.rs:99-150
+  // Evaluation schedule: a try is a full fused pass, or a loss-only pass
+  // completed (G, H, Σψ′) only if that try becomes the new iterate (both
+  // bit-identical). Non-ortho searches evaluate their tries in one multi-α pass
+  // (from try 1 when `multi_first`, else from try 2), which forms Y_α as Y + αZ
+  // and so agrees with per-try passes to rounding.
   const size_t n = nc_;
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
-  LsResult r{false, W_, S_, current_loss_, Mat(), false, 0};
+  LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false};
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
@@ -300,6 +303,55 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries) {  // c
       for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += alpha * direction.a[e];
     }
     r.w = matmul(transform, W_);
+    if (!ortho && !no_multi_ && (k == 1 || (k == 0 && multi_first))) {
+      // Non-ortho: Y_α = Y + α·Z is linear in α, so the remaining tries share
+      // one pass (see eval_loss_multi); only the accepted try is evaluated in full.
+      const size_t na = tries - k;
+      std::vector<double> alphas(na), ll(na * n), y2(na * n);
+      for (size_t j = 0; j < na; ++j) alphas[j] = j == 0 ? alpha : alphas[j - 1] / 2.0;
+      Mat wt = matmul(W_, P_);
+      Mat zt = matmul(matmul(direction, W_), P_);
+      if (ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
+                               alphas.data(), (int)na, ll.data(), y2.data())) {
+        ++last_evals_;
+        ++total_evals_;
+        EvalStats ls;
+        ls.nc = n;
+        ls.has_h = false;
+        ls.buf.assign(EvalStats::size(n, false), 0.0);
+        for (size_t j = 0; j < na; ++j) {
+          const double a = alphas[j];
+          if (j > 0) {
+            transform = Mat::eye(n);
+            for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += a * direction.a[e];
+            r.w = matmul(transform, W_);
+          }
+          std::memcpy(const_cast<double*>(ls.ll()), ll.data() + j * n, n * sizeof(double));
+          std::memcpy(const_cast<double*>(ls.y2()), y2.data() + j * n, n * sizeof(double));
+          r.tries = k + j + 1;
+          bool singular;
+          const double loss = loss_of(ls, r.w, signs_, &singular);
+          if (loss < current_loss_) {
+            evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
+            r.partial = false;
+            r.loss = loss_of(r.stats, r.w, signs_, &singular);
+            r.success = true;
+            r.step = scale(direction, a);
+            return r;
+          }
+          alpha = a / 2.0;
+        }
+        // no try accepted: the caller evaluates the last try in full if it keeps it
+        r.stats = ls;
+        r.partial = false;
+        r.needs_full = true;
+        bool singular;
+        r.loss = loss_of(ls, r.w, signs_, &singular);
+        r.step = scale(direction, alpha);
+        return r;
+      }
+      no_multi_ = true;  // evaluator cannot: per-try passes from now on
+    }
     if (k == 0 && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
@@ -404,15 +456,21 @@ bool Solver::step() {
     mem_.clear();
   }
   Mat direction = compute_direction(g, h, h_off, mem_, ortho);  // core.rs:334
-  LsResult res = line_search(direction, cfg_.ls_tries);
+  // non-ortho: all tries in one multi-α pass unless the last search accepted at try 1
+  LsResult res = line_search(direction, cfg_.ls_tries, !first_full_);
   const size_t first_tries = res.tries;
   const bool first_ok = res.success;
   first_full_ = res.success && res.tries == 1;
   if (!res.success) {  // core.rs:349-364
     mem_.clear();
-    res = line_search(scale(g, -1.0), 10);
+    res = line_search(scale(g, -1.0), 10, false);
   }
   if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
+  if (res.needs_full) {  // rejected multi-try search kept as the iterate
+    evaluate(res.w, &res.stats);
+    bool singular;
+    res.loss = loss_of(res.stats, res.w, signs_, &singular);
+  }
   if (trace_) {
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,

@@ -41,8 +41,8 @@ class Solver {
   void evaluate(const Mat& w_core, EvalStats* out);
   bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
   void complete(EvalStats* out);
-  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; };
-  LsResult line_search(const Mat& direction, size_t tries);
+  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full; };
+  LsResult line_search(const Mat& direction, size_t tries, bool multi_first);
   void init_core();
   Mat ica_par(const Mat& w_init);
   Mat jade(size_t max_iter, double tol);
@@ -87,6 +87,9 @@ class Solver {
   //                        accepted at try 1
   bool first_full_ = true;
   bool keep_y_ = false, split_first_ = false;
+  // Non-ortho searches evaluate tries >= 2 in one multi-α pass
+  // (Evaluator::eval_loss_multi) unless PICARD_NO_MULTI=1.
+  bool no_multi_ = false;
   bool trace_ = false;  // PICARD_TRACE=1: one stderr line per iteration (line-search tries)
 };
 

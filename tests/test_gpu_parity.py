@@ -96,6 +96,39 @@ def test_split_eval_bit_identical(pa, rng, n, dens, need_h):
         assert np.array_equal(done[k], full[k]), k
 
 
+@pytest.mark.parametrize("nc,nf", [(8, 8), (30, 30), (64, 64), (100, 100), (256, 256), (20, 70)])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("tanh", 0.6), ("exp", 0.5), ("cube", 1.0)])
+def test_multi_try_loss_pass(pa, rng, nc, nf, dens):
+    """Non-ortho line search in one pass: Σℓ, Σy² of (w + α_j z)(X − μ) for every try α_j
+    equal a separate pass at each try to 1e-12 relative (Y_j is formed as Y + α_j Z,
+    so they differ by rounding only). 13 tries exercise the 12-per-pass chunking."""
+    x = laplace_mix(rng, nf, 3001)
+    ctx = ctx_with(pa, x)
+    w = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    z = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    d = pa.DensityType(["tanh", "exp", "cube"].index(dens[0]), dens[1])
+    alphas = 0.5 ** np.arange(1, 14)
+    ll, y2 = ctx.eval_loss_multi(w, z, alphas, mu, d)
+    for j, a in enumerate(alphas):
+        ref = ctx.eval(w + a * z, mu, d)
+        assert rel_err(ll[j], ref["ll"]) <= TOL, j
+        assert rel_err(y2[j], ref["y2"]) <= TOL, j
+
+
+def test_multi_try_schedule_matches_per_try(pa, rng, monkeypatch):
+    """A non-ortho fit with the one-pass line search takes the same iterations as one
+    with a pass per try (PICARD_NO_MULTI=1) and lands on the same unmixing."""
+    x = laplace_mix(rng, 40, 20000)
+    cfg = dict(ortho=False, extended=True, max_iter=200, random_state=3)
+    r1 = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg))
+    monkeypatch.setenv("PICARD_NO_MULTI", "1")
+    r2 = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg))
+    assert r1.converged and r2.converged
+    assert abs(r1.n_iterations - r2.n_iterations) <= 2
+    assert np.max(np.abs(r1.unmixing - r2.unmixing)) <= 1e-6
+
+
 def test_eval_deterministic(pa, rng):
     x = laplace_mix(rng, 64, 20000)
     ctx = ctx_with(pa, x)
