@@ -197,6 +197,115 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 }
 
 // ---------------------------------------------------------------------------
+// Per-lane row accumulators of the register-resident kernels (fused, loss-only,
+// completion). Every term is arranged to vanish EXACTLY at y = 0, the value a
+// padded sample (zero X̃ column) produces, so no per-element validity masks are
+// needed; the per-sample constants are restored once per row in finalize_row:
+//   tanh  Σψ′ = α·(n − Σ th²)               (ψ′ = α(1 − th²))
+//         Σℓ  = Σ|y| + (n·ln2 + ln Π(1 + em/2))/α   (ℓ = |y| + ln(2 + em)/α)
+//         the product replaces one fp64 log per element by one multiply; it is
+//         kept as mantissa × 2^e (renormalised once per block) and its log is
+//         taken once per lane
+//   exp   Σψ′ = n + Σ(em − α y² k),  Σℓ = −(n + Σ em)/α   (k = e^{−αy²/2} = 1 + em)
+//   cube  Σψ′ = 3·Σy²,  Σℓ = Σ y⁴/4
+// All kernels of this family share these formulas and the sample → lane map,
+// so their sums stay bit-identical to each other.
+// ---------------------------------------------------------------------------
+struct RowAcc {
+  double d = 0.0, l = 0.0, q = 0.0;  // raw Σψ′ term, raw Σℓ term, Σy²
+  double p = 1.0;                    // tanh: Π (1 + em/2), mantissa
+  int e = 0;                         //       … and binary exponent
+};
+
+// ψ (and ψ′ if NEED_D) for one element; accumulates the row terms.
+template <int DENS, bool NEED_D>
+__device__ __forceinline__ void density_acc(double y, double alpha, RowAcc& a, double& psi, double& dpsi) {
+  a.q = __builtin_fma(y, y, a.q);
+  if constexpr (DENS == DENS_TANH) {
+    const double em = tanh_em(y, alpha);  // e^{-2α|y|} − 1 ∈ (−1, 0], 0 at y = 0
+    const double th = copysign(fm::div_nr(-em, 2.0 + em), alpha * y);
+    psi = th;
+    a.d = __builtin_fma(th, th, a.d);
+    if constexpr (NEED_D) dpsi = alpha * __builtin_fma(-th, th, 1.0);
+    a.l += fabs(y);
+    a.p *= __builtin_fma(em, 0.5, 1.0);  // ∈ (0.5, 1], exactly 1 at y = 0
+  } else if constexpr (DENS == DENS_EXP) {
+    const double y2 = y * y;
+    double em_r, sc;
+    fm::exp_parts(fmax(-alpha / 2.0 * y2, -708.0), em_r, sc);
+    const double k = __builtin_fma(sc, em_r, sc);
+    const double em = k - 1.0;  // exactly 0 at y = 0
+    const double ay2k = (alpha * y2) * k;
+    psi = y * k;
+    a.d += em - ay2k;
+    if constexpr (NEED_D) dpsi = k - ay2k;
+    a.l += em;
+  } else if constexpr (DENS == DENS_CUBE) {
+    const double y2 = y * y;
+    psi = y2 * y;
+    if constexpr (NEED_D) dpsi = 3.0 * y2;
+    a.l = __builtin_fma(y2, y2, a.l);
+  } else {  // LINEAR: ψ = y turns G_raw into the Gram Σ y yᵀ; row terms unused
+    psi = y;
+    if constexpr (NEED_D) dpsi = 1.0;
+  }
+}
+
+// ℓ terms only (line-search tries): identical arithmetic to density_acc's ℓ part
+template <int DENS>
+__device__ __forceinline__ void loss_acc(double y, double alpha, RowAcc& a) {
+  a.q = __builtin_fma(y, y, a.q);
+  if constexpr (DENS == DENS_TANH) {
+    const double em = tanh_em(y, alpha);
+    a.l += fabs(y);
+    a.p *= __builtin_fma(em, 0.5, 1.0);
+  } else if constexpr (DENS == DENS_EXP) {
+    const double y2 = y * y;
+    double em_r, sc;
+    fm::exp_parts(fmax(-alpha / 2.0 * y2, -708.0), em_r, sc);
+    a.l += __builtin_fma(sc, em_r, sc) - 1.0;
+  } else if constexpr (DENS == DENS_CUBE) {
+    const double y2 = y * y;
+    a.l = __builtin_fma(y2, y2, a.l);
+  }
+}
+
+// once per block (≤ 16 factors ≥ 1/2 since the last call: no underflow)
+template <int DENS>
+__device__ __forceinline__ void acc_renorm(RowAcc& a) {
+  if constexpr (DENS == DENS_TANH) {
+    int ex;
+    a.p = frexp(a.p, &ex);
+    a.e += ex;
+  }
+}
+
+// per-lane raw Σℓ term (before the cross-lane sums)
+template <int DENS>
+__device__ __forceinline__ double acc_ll(const RowAcc& a, double inv_alpha) {
+  if constexpr (DENS == DENS_TANH)
+    return __builtin_fma(__builtin_fma((double)a.e, fm::LN2, log(a.p)), inv_alpha, a.l);
+  else
+    return a.l;
+}
+
+// per-lane raw Σψ′ term (cube: ψ′ = 3y², so it is Σy² itself)
+template <int DENS>
+__device__ __forceinline__ double acc_dpsi(const RowAcc& a) {
+  if constexpr (DENS == DENS_CUBE) return a.q;
+  else return a.d;
+}
+
+// raw row sum → statistic (c: 0 Σψ′, 1 Σℓ, 2 Σy²), n = valid samples of this shard
+__host__ __device__ inline double finalize_row(int dens, double alpha, double n, int c, double raw) {
+  if (c == 2) return raw;
+  if (dens == DENS_TANH) return c == 0 ? alpha * (n - raw) : raw + n * (0x1.62e42fefa39efp-1 / alpha);
+  if (dens == DENS_EXP) return c == 0 ? n + raw : -(n + raw) / alpha;
+  if (dens == DENS_CUBE) return c == 0 ? 3.0 * raw : 0.25 * raw;
+  return c == 0 ? n : 0.0;  // LINEAR (Gram): unused
+}
+
+// ---------------------------------------------------------------------------
 // The fused pass. NB = 16-row blocks of Y (nc ≤ 16·NB), 8 waves.
 // Block = TB = 16·(8/NB) samples; each wave owns one 16×16 Yᵀ tile of it.
 // ---------------------------------------------------------------------------
@@ -221,11 +330,11 @@ __host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
 }
 
 // Software-pipelined over blocks with ONE barrier per block: iteration b
-// runs the Y stage of block b+1 (four interleaved MFMA chains) next to the G
-// stage of block b (GI·GJ independent accumulators) in one basic block, so
-// the chains' latency hides under independent MFMAs; X tiles and ψ/Y images
-// are double-buffered. Loads/stores of X use clamped block indices and
-// selects instead of branches (the last iteration is peeled).
+// runs the Y stage of block b+1 (one MFMA accumulation chain) next to the G
+// stage of block b (GI·GJ independent accumulators) in one basic block; X
+// tiles and ψ/Y images are double-buffered. Loads of X use clamped block
+// indices instead of branches (the last iteration is peeled); the row sums
+// need no validity masks (RowAcc).
 // X rows are padded to ldx ≡ 0 (mod 128) so a TB-sample tile never crosses a row end.
 template <int NB, bool NEED_H, int DENS>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
@@ -266,79 +375,76 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   for (int i = 0; i < GI; ++i)
 #pragma unroll
     for (int j = 0; j < GJ; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
-  double rs_dpsi = 0.0, rs_ll = 0.0, rs_y2 = 0.0;
+  RowAcc racc;
 
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint64_t b_last = b_end - 1;
 
-  // per-thread X staging slots: row k, sample pair t (fixed for the launch)
+  // per-thread X staging slots: row k, sample pair t (fixed for the launch).
+  // Rows k ≥ nf re-read row 0: their W columns are zero, so they add exactly 0.
   int xk[PRE], xt[PRE];
   double xmu[PRE];
-  bool xrow_ok[PRE];
+  const double* xsrc[PRE];
 #pragma unroll
   for (int p = 0; p < PRE; ++p) {
     const int e = tid + p * FUSED_THREADS;
     xk[p] = e / (TB / 2);
     xt[p] = 2 * (e % (TB / 2));
-    xrow_ok[p] = xk[p] < nf;
-    xmu[p] = (xrow_ok[p] && mu) ? mu[xk[p]] : 0.0;
+    const bool ok = xk[p] < nf;
+    xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
+    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
   }
   // two register sets for the X prefetch: the set stored in iteration b was
   // loaded at the START of iteration b−1, a full iteration of latency hiding
   double2 preA[PRE], preB[PRE];
   auto load_x = [&](uint64_t b, double2 (&pre)[PRE]) {  // b ≤ b_last: always a valid address
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) {
-      const int k = xrow_ok[p] ? xk[p] : 0;
-      pre[p] = *reinterpret_cast<const double2*>(X + (size_t)k * ldx + b * TB + xt[p]);
-    }
+    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * TB);
   };
+  // X̃ = X − μ into LDS; samples past n_local become exact zeros (only the
+  // grid's last block can hold any: a uniform branch, no per-element selects)
   auto store_x = [&](uint64_t b, double* xs, const double2 (&pre)[PRE]) {
+    if (b * TB + TB <= n_local) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) {
-      const uint64_t tg = b * TB + xt[p];
-      double2 v;
-      v.x = (xrow_ok[p] && tg < n_local) ? pre[p].x - xmu[p] : 0.0;
-      v.y = (xrow_ok[p] && tg + 1 < n_local) ? pre[p].y - xmu[p] : 0.0;
-      *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
-    }
-  };
-  // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over NFP, as two chains
-  // (same four-chain order as k_eval_loss, so both produce bit-identical Y)
-  auto y_stage = [&](const double* xs) {
-    d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0}, yc = d4{0, 0, 0, 0}, yd = d4{0, 0, 0, 0};
-    const double* xrow = xs + (yts * NFP + lk) * 16 + lr;
-    if constexpr (KS >= 4) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ks += 4) {
-        ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
-        yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
-        yc = mfma(xrow[(4 * ks + 8) * 16], wf[ks + 2], yc);
-        yd = mfma(xrow[(4 * ks + 12) * 16], wf[ks + 3], yd);
+      for (int p = 0; p < PRE; ++p) {
+        const double2 v = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
+        *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
       }
     } else {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+      for (int p = 0; p < PRE; ++p) {
+        const uint64_t tg = b * TB + xt[p];
+        double2 v;
+        v.x = tg < n_local ? pre[p].x - xmu[p] : 0.0;
+        v.y = tg + 1 < n_local ? pre[p].y - xmu[p] : 0.0;
+        *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
+      }
     }
-    return (ya + yb) + (yc + yd);
   };
-  // density on the tile, row sums, hand-off of the ψ / y (/ ψ′) fragments
-  auto elementwise = [&](const d4& yv, uint64_t b, double* img) {
+  // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over NFP as ONE accumulation
+  // chain (back-to-back dependent fp64 MFMAs issue at full rate on gfx950:
+  // tools/microbench/mfma_chain.hip), in the same order as k_eval_loss
+  auto y_stage = [&](const double* xs) {
+    d4 ya = d4{0, 0, 0, 0};
+    const double* xrow = xs + (yts * NFP + lk) * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+    return ya;
+  };
+  // density on the tile, row terms, hand-off of the ψ / y (/ ψ′) fragments
+  auto elementwise = [&](const d4& yv, double* img) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const double y = yv[r];
-      double psi, dpsi, ll;
-      density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
-      const bool valid = b * TB + yts * 16 + 4 * r + lk < n_local;
-      rs_dpsi += valid ? dpsi : 0.0;
-      rs_ll += valid ? ll : 0.0;
-      rs_y2 = __builtin_fma(y, y, rs_y2);  // y = 0 exactly for samples past the end (zero X columns)
+      double psi, dpsi;
+      density_acc<DENS, NEED_H>(y, alpha, racc, psi, dpsi);
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
       img[f] = psi;
       img[S::FRAGS + f] = y;
       if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi;
     }
+    acc_renorm<DENS>(racc);
   };
   // G stage: G_raw[i-blocks][j-blocks] += ψ · Yᵀ (H_raw += ψ′ · (Y∘Y)ᵀ) over one block
   auto g_stage = [&](const double* img) {
@@ -372,17 +478,18 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     store_x(b_begin, xs0, preA);
     load_x(clampb(b_begin + 1), preA);
     __syncthreads();
-    elementwise(y_stage(xs0), b_begin, img0);
+    elementwise(y_stage(xs0), img0);
     store_x(clampb(b_begin + 1), xs0 + XS, preA);
     load_x(clampb(b_begin + 2), preA);
     __syncthreads();
     // iteration b: Y stage of b+1 ‖ G stage of b; X(b+2) (loaded a full iteration
-    // ago) → xs[cur]; X(b+3) requested at the top
+    // ago) → xs[cur]; X(b+3) requested at the top. A clamped (repeated) block is
+    // never consumed twice: its Y stage is the peeled tail's, which is skipped.
     auto iter = [&](uint64_t b, int cur, double2 (&use)[PRE], double2 (&fill)[PRE]) {
       load_x(clampb(b + 3), fill);
       const d4 yv = y_stage(xs0 + (cur ^ 1) * XS);     // block b+1
       g_stage(img0 + cur * NIMG * S::FRAGS);           // block b
-      elementwise(yv, b + 1, img0 + (cur ^ 1) * NIMG * S::FRAGS);
+      elementwise(yv, img0 + (cur ^ 1) * NIMG * S::FRAGS);
       store_x(clampb(b + 2), xs0 + cur * XS, use);
       __syncthreads();
     };
@@ -441,6 +548,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     __syncthreads();
   }
   // row sums: over the 4 lane groups, then over the TS waves of one row block
+  double rs_dpsi = acc_dpsi<DENS>(racc), rs_ll = acc_ll<DENS>(racc, inv_alpha), rs_y2 = racc.q;
   rs_dpsi += __shfl_xor(rs_dpsi, 16); rs_dpsi += __shfl_xor(rs_dpsi, 32);
   rs_ll += __shfl_xor(rs_ll, 16);     rs_ll += __shfl_xor(rs_ll, 32);
   rs_y2 += __shfl_xor(rs_y2, 16);     rs_y2 += __shfl_xor(rs_y2, 32);
@@ -485,35 +593,43 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
   double wf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) wf[ks] = Wp[(yi * 16 + lr) * NFP + 4 * ks + lk];
-  double rs_ll = 0.0, rs_y2 = 0.0;
+  RowAcc racc;
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint64_t b_last = b_end - 1;
   int xk[PRE], xt[PRE];
   double xmu[PRE];
-  bool xrow_ok[PRE];
+  const double* xsrc[PRE];
 #pragma unroll
-  for (int p = 0; p < PRE; ++p) {
+  for (int p = 0; p < PRE; ++p) {  // same staging map as k_eval_fused (rows ≥ nf: zero W columns)
     const int e = tid + p * FUSED_THREADS;
     xk[p] = e / (TB / 2);
     xt[p] = 2 * (e % (TB / 2));
-    xrow_ok[p] = xk[p] < nf;
-    xmu[p] = (xrow_ok[p] && mu) ? mu[xk[p]] : 0.0;
+    const bool ok = xk[p] < nf;
+    xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
+    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
   }
   double2 pre[PRE];
   auto load_x = [&](uint64_t b) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p)
-      pre[p] = *reinterpret_cast<const double2*>(X + (size_t)(xrow_ok[p] ? xk[p] : 0) * ldx + b * TB + xt[p]);
+    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * TB);
   };
   auto store_x = [&](uint64_t b, double* xs) {
+    if (b * TB + TB <= n_local) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) {
-      const uint64_t tg = b * TB + xt[p];
-      double2 v;
-      v.x = (xrow_ok[p] && tg < n_local) ? pre[p].x - xmu[p] : 0.0;
-      v.y = (xrow_ok[p] && tg + 1 < n_local) ? pre[p].y - xmu[p] : 0.0;
-      *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
+      for (int p = 0; p < PRE; ++p) {
+        const double2 v = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
+        *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        const uint64_t tg = b * TB + xt[p];
+        double2 v;
+        v.x = tg < n_local ? pre[p].x - xmu[p] : 0.0;
+        v.y = tg + 1 < n_local ? pre[p].y - xmu[p] : 0.0;
+        *reinterpret_cast<double2*>(xs + ((xt[p] >> 4) * NFP + xk[p]) * 16 + (xt[p] & 15)) = v;
+      }
     }
   };
   auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
@@ -526,35 +642,23 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
     // Y stage and the density math of block b, which hide its latency
     for (uint64_t b = b_begin; b < b_end; ++b) {
       load_x(clampb(b + 1));
-      // four independent chains: no G stage here to hide the MFMA latency behind
-      d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0}, yc = d4{0, 0, 0, 0}, yd = d4{0, 0, 0, 0};
+      d4 yv = d4{0, 0, 0, 0};  // one chain, same order as k_eval_fused's Y stage
       const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
-      if constexpr (KS >= 4) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ks += 4) {
-          ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
-          yb = mfma(xrow[(4 * ks + 4) * 16], wf[ks + 1], yb);
-          yc = mfma(xrow[(4 * ks + 8) * 16], wf[ks + 2], yc);
-          yd = mfma(xrow[(4 * ks + 12) * 16], wf[ks + 3], yd);
-        }
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
-      }
-      const d4 yv = (ya + yb) + (yc + yd);
+      for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const double y = yv[r];
-        const double ll = density_loss<DENS>(y, alpha, inv_alpha);
-        rs_ll += (b * TB + yts * 16 + 4 * r + lk < n_local) ? ll : 0.0;
-        rs_y2 = __builtin_fma(y, y, rs_y2);
+        loss_acc<DENS>(y, alpha, racc);
         if constexpr (STORE) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = y;
       }
+      acc_renorm<DENS>(racc);
       store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
       __syncthreads();
       cur ^= 1;
     }
   }
+  double rs_ll = acc_ll<DENS>(racc, inv_alpha), rs_y2 = racc.q;
   rs_ll += __shfl_xor(rs_ll, 16); rs_ll += __shfl_xor(rs_ll, 32);
   rs_y2 += __shfl_xor(rs_y2, 16); rs_y2 += __shfl_xor(rs_y2, 32);
   double* rsb = xs0;  // [TS][NCP][2]
@@ -596,7 +700,8 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
   for (int i = 0; i < GI; ++i)
 #pragma unroll
     for (int j = 0; j < GJ; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
-  double rs_dpsi = 0.0;
+  RowAcc racc;
+  (void)n_local;
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint64_t b_last = b_end - 1;
@@ -606,14 +711,12 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
     for (int r = 0; r < 4; ++r) v[r] = ybuf[((b * 8 + wave) * 4 + r) * 64 + lane];
     return v;
   };
-  auto elementwise = [&](const d4& yv, uint64_t b, double* img) {
+  auto elementwise = [&](const d4& yv, double* img) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const double y = yv[r];
-      double psi, dpsi, ll;
-      density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
-      (void)ll;
-      rs_dpsi += (b * TB + yts * 16 + 4 * r + lk < n_local) ? dpsi : 0.0;
+      double psi, dpsi;
+      density_acc<DENS, NEED_H>(y, alpha, racc, psi, dpsi);
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
       img[f] = psi;
       img[S::FRAGS + f] = y;
@@ -645,7 +748,7 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
   };
   if (b_begin < b_end) {
     auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
-    elementwise(load_y(b_begin), b_begin, img0);
+    elementwise(load_y(b_begin), img0);
     d4 pre = load_y(clampb(b_begin + 1));
     __syncthreads();
     int cur = 0;
@@ -653,7 +756,7 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
       const d4 yv = pre;
       pre = load_y(clampb(b + 2));
       g_stage(img0 + cur * NIMG * S::FRAGS);
-      elementwise(yv, b + 1, img0 + (cur ^ 1) * NIMG * S::FRAGS);
+      elementwise(yv, img0 + (cur ^ 1) * NIMG * S::FRAGS);
       __syncthreads();
       cur ^= 1;
     }
@@ -698,6 +801,7 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
     }
     __syncthreads();
   }
+  double rs_dpsi = acc_dpsi<DENS>(racc);
   rs_dpsi += __shfl_xor(rs_dpsi, 16); rs_dpsi += __shfl_xor(rs_dpsi, 32);
   double* rsb = img0 + 2 * NIMG * S::FRAGS - TS * NCP;  // [TS][NCP] at the end of the image area
   __syncthreads();
@@ -712,14 +816,15 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
 }
 
 // out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets (fixed order)
+// then finalize_row(dens, α, n, c0 + c, ·) unless dens < 0 (already final)
 __global__ void k_reduce_rows(const double* __restrict__ partials, int nwg, size_t pstride, size_t poff, int ncp,
-                              int nc, int nsets, double* __restrict__ out) {
+                              int nc, int nsets, double* __restrict__ out, int dens, double alpha, double n, int c0) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nsets * nc) return;
   const int c = e / nc, row = e % nc;
   double s = 0.0;
   for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + poff + (size_t)c * ncp + row];
-  out[e] = s;
+  out[e] = dens < 0 ? s : finalize_row(dens, alpha, n, c0 + c, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1076,7 +1181,7 @@ __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, con
 // Fixed-order sum of per-workgroup partials into the compact stats layout
 // [G nc×nc | H nc×nc | Σψ′ nc | Σℓ nc | Σy² nc].
 __global__ void k_reduce(const double* __restrict__ partials, int nwg, size_t pstride, int ncp, int nc,
-                         bool need_h, double* __restrict__ stats) {
+                         bool need_h, double* __restrict__ stats, int dens, double alpha, double n) {
   const size_t nsq = (size_t)nc * nc;
   const size_t total = (need_h ? 2 : 1) * nsq + 3 * (size_t)nc;
   const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -1090,7 +1195,8 @@ __global__ void k_reduce(const double* __restrict__ partials, int nwg, size_t ps
   }
   double s = 0.0;
   for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + src];
-  stats[e] = s;
+  const size_t mats = (need_h ? 2 : 1) * nsq;
+  stats[e] = e < mats ? s : finalize_row(dens, alpha, n, (int)((e - mats) / nc), s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1492,7 +1598,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t total = EvalStats::size(nc, H);
-    k_reduce<<<(total + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st);
+    k_reduce<<<(total + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
+                                                      (double)n_local_);
     HIP_OK(hipGetLastError());
   }
 
@@ -1507,8 +1614,13 @@ struct DeviceCtx : Evaluator {
   }
   template <int NB>
   void dispatch_h(bool h, int dens, int nfp, const double* dmu, double alpha, double* st, size_t nc) {
-    if (h) dispatch_dens<NB, true>(dens, nfp, dmu, alpha, st, nc);
-    else dispatch_dens<NB, false>(dens, nfp, dmu, alpha, st, nc);
+    if constexpr (NB == 8) {  // H at nc > 64 goes to the tiled path (register budget)
+      if (h) throw computation_error("fused pass with H needs nc <= 64");
+      dispatch_dens<NB, false>(dens, nfp, dmu, alpha, st, nc);
+    } else {
+      if (h) dispatch_dens<NB, true>(dens, nfp, dmu, alpha, st, nc);
+      else dispatch_dens<NB, false>(dens, nfp, dmu, alpha, st, nc);
+    }
   }
 
   void run_eval(const double* w, size_t nc, const double* mu, int dens, double alpha, bool need_h, double* stats_host) {
@@ -1600,7 +1712,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventRecord(ev[2], stream));
     double* st = ensure(d_stats, cap_stats, (size_t)2 * na * nc);
     // st[(j·2 + c)·nc + row] = Σ_w part[w][(j·2 + c)·ncp + row]
-    k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st);
+    k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
+                                                                        -1, 0.0, 0.0, 0);
     HIP_OK(hipGetLastError());
     allreduce(st, (size_t)2 * na * nc);
     std::vector<double> h((size_t)2 * na * nc);
@@ -1783,7 +1896,8 @@ struct DeviceCtx : Evaluator {
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
-    k_reduce_rows<<<1, 512, 0, stream>>>(part, nwg, 2 * S::NCP, 0, S::NCP, (int)kept_nc_pending, 2, st_rows);
+    k_reduce_rows<<<1, 512, 0, stream>>>(part, nwg, 2 * S::NCP, 0, S::NCP, (int)kept_nc_pending, 2, st_rows, D, alpha,
+                                         (double)n_local_, 1);
     HIP_OK(hipGetLastError());
   }
   size_t kept_nc_pending = 0;
@@ -1803,7 +1917,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t nc = kept_nc;
     const size_t e1 = (H ? 2 : 1) * nc * nc + nc;  // [G | H | Σψ′]
-    k_reduce<<<(e1 + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st);
+    k_reduce<<<(e1 + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
+                                                   (double)n_local_);
     HIP_OK(hipGetLastError());
   }
 
