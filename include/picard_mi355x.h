@@ -144,8 +144,11 @@ uint64_t pc_ctx_t0(const pc_ctx* ctx);
 
 /* Operator boundary. All statistics are summed over every rank's shard
  * (one RCCL all-reduce per call when world_size > 1). */
-enum { PC_EVAL_NEED_H = 1u };
-/* stats = [G_raw (nc×nc) | H_raw (nc×nc, only with PC_EVAL_NEED_H) | Σψ′ (nc) | Σℓ (nc) | Σy² (nc)] */
+enum { PC_EVAL_NEED_H = 1u, PC_EVAL_SKIP_Y2 = 2u };
+/* stats = [G_raw (nc×nc) | H_raw (nc×nc, only with PC_EVAL_NEED_H) | Σψ′ (nc) | Σℓ (nc) | Σy² (nc)].
+ * PC_EVAL_SKIP_Y2 (ignored with NEED_H): Σy² is not accumulated and reads 0 —
+ * the orthogonal solver never uses it (core.rs:221 computes Y∘Y, read only at
+ * :274 and by the extended non-orthogonal loss), saving one fp64 op per element. */
 int pc_ctx_eval(pc_ctx* ctx, const double* w /* nc × n_features */, uint64_t nc,
                 const double* mu /* n_features or NULL */, pc_density density, uint32_t flags,
                 double* stats, char* err, size_t errlen);

@@ -517,15 +517,19 @@ class DeviceContext:
         lib.pc_ctx_download(self.h, _ptr(out))
         return out
 
-    def eval(self, w, mu=None, density: DensityType = DensityType(), need_h: bool = False) -> dict:
+    def eval(self, w, mu=None, density: DensityType = DensityType(), need_h: bool = False,
+             need_y2: bool = True) -> dict:
+        """pc_ctx_eval: one fused pass. need_y2=False (PC_EVAL_SKIP_Y2) leaves Σy² at 0
+        unless need_h (the orthogonal solver never reads it)."""
         w = _c64(w)
         nc = w.shape[0]
         mu_a = _c64(mu) if mu is not None else None
         n = (2 if need_h else 1) * nc * nc + 3 * nc
         st = np.empty(n)
         err = _errbuf()
+        flags = (1 if need_h else 0) | (0 if need_y2 else 2)
         _raise(lib.pc_ctx_eval(self.h, _ptr(w), nc, _ptr(mu_a) if mu_a is not None else None, density._c(),
-                               1 if need_h else 0, _ptr(st), err, len(err)), err)
+                               flags, _ptr(st), err, len(err)), err)
         o = nc * nc
         out = {"G": st[:o].reshape(nc, nc)}
         if need_h:
@@ -544,7 +548,8 @@ class DeviceContext:
         out["dpsi"], out["ll"], out["y2"] = st[o:o + nc], st[o + nc:o + 2 * nc], st[o + 2 * nc:o + 3 * nc]
         return out
 
-    def eval_split(self, w, mu=None, density: DensityType = DensityType(), need_h: bool = False):
+    def eval_split(self, w, mu=None, density: DensityType = DensityType(), need_h: bool = False,
+                   need_y2: bool = True):
         """pc_ctx_eval_loss then pc_ctx_eval_complete; returns (loss-only stats, kept, completed stats)."""
         w = _c64(w)
         nc = w.shape[0]
@@ -553,8 +558,9 @@ class DeviceContext:
         st = np.full(n, np.nan)
         kept = C.c_int32()
         err = _errbuf()
+        flags = (1 if need_h else 0) | (0 if need_y2 else 2)
         _raise(lib.pc_ctx_eval_loss(self.h, _ptr(w), nc, _ptr(mu_a) if mu_a is not None else None, density._c(),
-                                    1 if need_h else 0, _ptr(st), C.byref(kept), err, len(err)), err)
+                                    flags, _ptr(st), C.byref(kept), err, len(err)), err)
         loss_only = st.copy()
         if kept.value:
             _raise(lib.pc_ctx_eval_complete(self.h, density._c(), 1 if need_h else 0, _ptr(st), err, len(err)), err)

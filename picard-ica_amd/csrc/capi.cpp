@@ -305,6 +305,7 @@ int pc_ctx_eval(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_de
   return guarded(err, errlen, [&] {
     if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
+    c->ev->want_y2 = (flags & PC_EVAL_SKIP_Y2) == 0;
     device_ctx_raw_eval(c->ev.get(), w, nc, mu, d.kind, d.alpha, (flags & PC_EVAL_NEED_H) != 0, stats);
   });
 }
@@ -315,6 +316,7 @@ int pc_ctx_eval_loss(pc_ctx* c, const double* w, uint64_t nc, const double* mu, 
     if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
     const bool h = (flags & PC_EVAL_NEED_H) != 0;
+    c->ev->want_y2 = (flags & PC_EVAL_SKIP_Y2) == 0;
     EvalStats st;
     *kept = c->ev->eval_loss(w, nc, mu, d, h, &st) ? 1 : 0;
     const size_t off = *kept ? st.buf.size() - 2 * nc : 0;  // kept: only [Σℓ | Σy²] are written

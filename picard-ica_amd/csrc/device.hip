@@ -217,60 +217,137 @@ struct RowAcc {
   int e = 0;                         //       … and binary exponent
 };
 
-// ψ (and ψ′ if NEED_D) for one element; accumulates the row terms.
-template <int DENS, bool NEED_D>
-__device__ __forceinline__ void density_acc(double y, double alpha, RowAcc& a, double& psi, double& dpsi) {
-  a.q = __builtin_fma(y, y, a.q);
-  if constexpr (DENS == DENS_TANH) {
-    const double em = tanh_em(y, alpha);  // e^{-2α|y|} − 1 ∈ (−1, 0], 0 at y = 0
-    const double th = copysign(fm::div_nr(-em, 2.0 + em), alpha * y);
-    psi = th;
-    a.d = __builtin_fma(th, th, a.d);
-    if constexpr (NEED_D) dpsi = alpha * __builtin_fma(-th, th, 1.0);
-    a.l += fabs(y);
-    a.p *= __builtin_fma(em, 0.5, 1.0);  // ∈ (0.5, 1], exactly 1 at y = 0
-  } else if constexpr (DENS == DENS_EXP) {
-    const double y2 = y * y;
-    double em_r, sc;
-    fm::exp_parts(fmax(-alpha / 2.0 * y2, -708.0), em_r, sc);
-    const double k = __builtin_fma(sc, em_r, sc);
-    const double em = k - 1.0;  // exactly 0 at y = 0
-    const double ay2k = (alpha * y2) * k;
-    psi = y * k;
-    a.d += em - ay2k;
-    if constexpr (NEED_D) dpsi = k - ay2k;
-    a.l += em;
-  } else if constexpr (DENS == DENS_CUBE) {
-    const double y2 = y * y;
-    psi = y2 * y;
-    if constexpr (NEED_D) dpsi = 3.0 * y2;
-    a.l = __builtin_fma(y2, y2, a.l);
-  } else {  // LINEAR: ψ = y turns G_raw into the Gram Σ y yᵀ; row terms unused
-    psi = y;
-    if constexpr (NEED_D) dpsi = 1.0;
+// e^x for NW independent x ∈ [−708, 0] as sc·(1 + emr), sc = 2^k, |r| ≤ ln2/2,
+// written step-interleaved so the NW dependent FMA chains overlap (left to
+// itself the compiler emits them one after another). Rounding to k uses the
+// 1.5·2^52 shifter (its low word IS k, so 2^k is built with one integer op);
+// the reduction r = x − k·ln2 is a single fma: its error |k|·2^-56·e^x stays
+// ≤ 1.2e-17 absolute for x ≤ 0, and is 0 for k = 0 (small |y|).
+template <int NW>
+__device__ __forceinline__ void exp_n(const double* x, double* emr, double* sc) {
+  constexpr double SHIFT = 0x1.8p52;
+  double t[NW], r[NW], p[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t[i] = __builtin_fma(x[i], fm::LOG2E, SHIFT);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r[i] = __builtin_fma(-(t[i] - SHIFT), fm::LN2, x[i]);
+  constexpr double C[10] = {0x1.af389ecfc4b9cp-26, 0x1.28917c89a43a7p-22, 0x1.71de0db2f6b19p-19,
+                            0x1.a019b9149a41cp-16, 0x1.a01a01a7c2efep-13, 0x1.6c16c17889ef1p-10,
+                            0x1.11111111109b5p-7,  0x1.5555555553d68p-5,  0x1.5555555555556p-3,
+                            0x1.0000000000001p-1};
+#pragma unroll
+  for (int i = 0; i < NW; ++i) p[i] = __builtin_fma(C[0], r[i], C[1]);
+#pragma unroll
+  for (int c = 2; c < 10; ++c)
+#pragma unroll
+    for (int i = 0; i < NW; ++i) p[i] = __builtin_fma(p[i], r[i], C[c]);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    emr[i] = __builtin_fma(r[i] * r[i], p[i], r[i]);
+    const int k = __double2loint(t[i]);
+    sc[i] = __hiloint2double((k + 1023) << 20, 0);
   }
 }
 
-// ℓ terms only (line-search tries): identical arithmetic to density_acc's ℓ part
-template <int DENS>
-__device__ __forceinline__ void loss_acc(double y, double alpha, RowAcc& a) {
-  a.q = __builtin_fma(y, y, a.q);
-  if constexpr (DENS == DENS_TANH) {
-    const double em = tanh_em(y, alpha);
-    a.l += fabs(y);
-    a.p *= __builtin_fma(em, 0.5, 1.0);
-  } else if constexpr (DENS == DENS_EXP) {
-    const double y2 = y * y;
-    double em_r, sc;
-    fm::exp_parts(fmax(-alpha / 2.0 * y2, -708.0), em_r, sc);
-    a.l += __builtin_fma(sc, em_r, sc) - 1.0;
-  } else if constexpr (DENS == DENS_CUBE) {
-    const double y2 = y * y;
-    a.l = __builtin_fma(y2, y2, a.l);
+// ψ (and ψ′ if NEED_D) of one 4-element fragment, NW elements interleaved at a
+// time (register budget); accumulates the row terms in element order, so the
+// sums do not depend on NW. Σy² only if NEED_Q (the reference uses Y∘Y only in
+// non-orthogonal mode; cube needs it for Σψ′). m2a = −2α.
+// th = −em/(2+em) uses one Newton step on v_rcp_f64 (≲ 10 ulp).
+template <int DENS, bool NEED_D, bool NEED_Q, int NW = 4>
+__device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m2a, RowAcc& a, double (&psi)[4],
+                                             double (&dpsi)[4]) {
+  if constexpr (NEED_Q || DENS == DENS_CUBE)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.q = __builtin_fma(y[i], y[i], a.q);
+#pragma unroll
+  for (int g = 0; g < 4; g += NW) {
+    if constexpr (DENS == DENS_TANH) {
+      double x[NW], emr[NW], sc[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) x[i] = fmax(m2a * fabs(y[g + i]), -708.0);  // = −2|αy| exactly (α > 0)
+      exp_n<NW>(x, emr, sc);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const double em = __builtin_fma(sc[i], emr[i], sc[i] - 1.0);  // e^{-2α|y|} − 1 ∈ (−1, 0]
+        const double th = copysign(-em * fm::rcp_nr1(2.0 + em), y[g + i]);
+        psi[g + i] = th;
+        a.d = __builtin_fma(th, th, a.d);
+        if constexpr (NEED_D) dpsi[g + i] = alpha * __builtin_fma(-th, th, 1.0);
+        a.l += fabs(y[g + i]);
+        a.p *= __builtin_fma(em, 0.5, 1.0);  // ∈ (0.5, 1], exactly 1 at y = 0
+      }
+    } else if constexpr (DENS == DENS_EXP) {
+      double x[NW], emr[NW], sc[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) x[i] = fmax(-alpha / 2.0 * (y[g + i] * y[g + i]), -708.0);
+      exp_n<NW>(x, emr, sc);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const double y2 = y[g + i] * y[g + i];
+        const double k = __builtin_fma(sc[i], emr[i], sc[i]);
+        const double em = k - 1.0;  // exactly 0 at y = 0
+        const double ay2k = (alpha * y2) * k;
+        psi[g + i] = y[g + i] * k;
+        a.d += em - ay2k;
+        if constexpr (NEED_D) dpsi[g + i] = k - ay2k;
+        a.l += em;
+      }
+    } else if constexpr (DENS == DENS_CUBE) {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const double y2 = y[g + i] * y[g + i];
+        psi[g + i] = y2 * y[g + i];
+        if constexpr (NEED_D) dpsi[g + i] = 3.0 * y2;
+        a.l = __builtin_fma(y2, y2, a.l);
+      }
+    } else {  // LINEAR: ψ = y turns G_raw into the Gram Σ y yᵀ; row terms unused
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        psi[g + i] = y[g + i];
+        if constexpr (NEED_D) dpsi[g + i] = 1.0;
+      }
+    }
   }
 }
 
-// once per block (≤ 16 factors ≥ 1/2 since the last call: no underflow)
+// ℓ terms only (line-search tries): identical arithmetic to density_acc4's ℓ part
+template <int DENS, bool NEED_Q, int NW = 4>
+__device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a, RowAcc& a) {
+  if constexpr (NEED_Q || DENS == DENS_CUBE)  // as density_acc4 (cube's fused pass keeps Σy²)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.q = __builtin_fma(y[i], y[i], a.q);
+#pragma unroll
+  for (int g = 0; g < 4; g += NW) {
+    if constexpr (DENS == DENS_TANH) {
+      double x[NW], emr[NW], sc[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) x[i] = fmax(m2a * fabs(y[g + i]), -708.0);
+      exp_n<NW>(x, emr, sc);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const double em = __builtin_fma(sc[i], emr[i], sc[i] - 1.0);
+        a.l += fabs(y[g + i]);
+        a.p *= __builtin_fma(em, 0.5, 1.0);
+      }
+    } else if constexpr (DENS == DENS_EXP) {
+      double x[NW], emr[NW], sc[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) x[i] = fmax(-alpha / 2.0 * (y[g + i] * y[g + i]), -708.0);
+      exp_n<NW>(x, emr, sc);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) a.l += __builtin_fma(sc[i], emr[i], sc[i]) - 1.0;
+    } else if constexpr (DENS == DENS_CUBE) {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        const double y2 = y[g + i] * y[g + i];
+        a.l = __builtin_fma(y2, y2, a.l);
+      }
+    }
+  }
+}
+
+// every few blocks (≤ 64 factors ≥ 1/2 since the last call: no underflow)
 template <int DENS>
 __device__ __forceinline__ void acc_renorm(RowAcc& a) {
   if constexpr (DENS == DENS_TANH) {
@@ -305,6 +382,18 @@ __host__ __device__ inline double finalize_row(int dens, double alpha, double n,
   return c == 0 ? n : 0.0;  // LINEAR (Gram): unused
 }
 
+// density interleave widths (register budget: fused 256 VGPRs, split kernels 128)
+#ifndef PC_FUSED_NW
+#define PC_FUSED_NW 2
+#endif
+#ifndef PC_LOSS_NW
+#define PC_LOSS_NW 1
+#endif
+#ifndef PC_FROMY_NW
+#define PC_FROMY_NW 1
+#endif
+constexpr int FUSED_NW = PC_FUSED_NW, LOSS_NW = PC_LOSS_NW, FROMY_NW = PC_FROMY_NW;
+
 // ---------------------------------------------------------------------------
 // The fused pass. NB = 16-row blocks of Y (nc ≤ 16·NB), 8 waves.
 // Block = TB = 16·(8/NB) samples; each wave owns one 16×16 Yᵀ tile of it.
@@ -336,7 +425,7 @@ __host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
 // indices instead of branches (the last iteration is peeled); the row sums
 // need no validity masks (RowAcc).
 // X rows are padded to ldx ≡ 0 (mod 128) so a TB-sample tile never crosses a row end.
-template <int NB, bool NEED_H, int DENS>
+template <int NB, bool NEED_H, int DENS, bool NEED_Q>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf,
              const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
@@ -353,7 +442,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int yi = wave % NB, yts = wave / NB;
-  const double inv_alpha = 1.0 / alpha;
+  const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
 
   extern __shared__ double smem[];
   double* xs0 = smem;             // [2][TS][NFP][16]
@@ -434,17 +523,15 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   };
   // density on the tile, row terms, hand-off of the ψ / y (/ ψ′) fragments
   auto elementwise = [&](const d4& yv, double* img) {
+    double psi[4], dpsi[4];
+    density_acc4<DENS, NEED_H, NEED_Q, FUSED_NW>(yv, alpha, m2a, racc, psi, dpsi);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const double y = yv[r];
-      double psi, dpsi;
-      density_acc<DENS, NEED_H>(y, alpha, racc, psi, dpsi);
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
-      img[f] = psi;
-      img[S::FRAGS + f] = y;
-      if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi;
+      img[f] = psi[r];
+      img[S::FRAGS + f] = yv[r];
+      if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi[r];
     }
-    acc_renorm<DENS>(racc);
   };
   // G stage: G_raw[i-blocks][j-blocks] += ψ · Yᵀ (H_raw += ψ′ · (Y∘Y)ᵀ) over one block
   auto g_stage = [&](const double* img) {
@@ -490,6 +577,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       const d4 yv = y_stage(xs0 + (cur ^ 1) * XS);     // block b+1
       g_stage(img0 + cur * NIMG * S::FRAGS);           // block b
       elementwise(yv, img0 + (cur ^ 1) * NIMG * S::FRAGS);
+      if (cur) acc_renorm<DENS>(racc);  // every second block
       store_x(clampb(b + 2), xs0 + cur * XS, use);
       __syncthreads();
     };
@@ -576,7 +664,8 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 //                  the G (H) stage: the rest of the statistics of an accepted try.
 // A rejected try then costs ≈ half a fused pass.
 // ---------------------------------------------------------------------------
-template <int NB, int DENS, bool STORE>
+
+template <int NB, int DENS, bool STORE, bool NEED_Q>
 __global__ void __launch_bounds__(FUSED_THREADS, 4)
 k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf,
             const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
@@ -587,7 +676,7 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int yi = wave % NB, yts = wave / NB;
-  const double inv_alpha = 1.0 / alpha;
+  const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
   extern __shared__ double smem[];
   double* xs0 = smem;  // [2][TS][NFP][16]
   double wf[KS];
@@ -609,6 +698,9 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
     xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
     xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
   }
+  // one prefetch register set (128-VGPR budget): X(b+1) is requested at the top
+  // of iteration b — pinned there by a scheduling barrier — and consumed after
+  // the Y stage and the density math of block b, which hide its HBM latency
   double2 pre[PRE];
   auto load_x = [&](uint64_t b) {
 #pragma unroll
@@ -638,21 +730,19 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
     store_x(b_begin, xs0);
     __syncthreads();
     int cur = 0;
-    // iteration b: X(b+1) requested at the top, consumed (→ xs[cur^1]) after the
-    // Y stage and the density math of block b, which hide its latency
     for (uint64_t b = b_begin; b < b_end; ++b) {
       load_x(clampb(b + 1));
+      __builtin_amdgcn_sched_barrier(0);
       d4 yv = d4{0, 0, 0, 0};  // one chain, same order as k_eval_fused's Y stage
       const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
+      loss_acc4<DENS, NEED_Q, LOSS_NW>(yv, alpha, m2a, racc);
+      if constexpr (STORE)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double y = yv[r];
-        loss_acc<DENS>(y, alpha, racc);
-        if constexpr (STORE) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = y;
-      }
-      acc_renorm<DENS>(racc);
+        for (int r = 0; r < 4; ++r) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = yv[r];
+      if (cur) acc_renorm<DENS>(racc);  // every second block
+      __builtin_amdgcn_sched_barrier(0);  // consume X(b+1) only after the density math
       store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
       __syncthreads();
       cur ^= 1;
@@ -712,15 +802,14 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
     return v;
   };
   auto elementwise = [&](const d4& yv, double* img) {
+    double psi[4], dpsi[4];
+    density_acc4<DENS, NEED_H, false, FROMY_NW>(yv, alpha, -2.0 * alpha, racc, psi, dpsi);  // ℓ, Σy² terms unused
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const double y = yv[r];
-      double psi, dpsi;
-      density_acc<DENS, NEED_H>(y, alpha, racc, psi, dpsi);
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
-      img[f] = psi;
-      img[S::FRAGS + f] = y;
-      if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi;
+      img[f] = psi[r];
+      img[S::FRAGS + f] = yv[r];
+      if constexpr (NEED_H) img[2 * S::FRAGS + f] = dpsi[r];
     }
   };
   auto g_stage = [&](const double* img) {
@@ -1577,7 +1666,7 @@ struct DeviceCtx : Evaluator {
 
   static int pick_nb(size_t nc) { return nc <= 16 ? 1 : nc <= 32 ? 2 : nc <= 64 ? 4 : nc <= 128 ? 8 : 0; }
 
-  template <int NB, bool H, int D>
+  template <int NB, bool H, int D, bool Q>
   void launch_fused(int nfp, const double* dmu, double alpha, double* st, size_t nc) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
@@ -1587,7 +1676,7 @@ struct DeviceCtx : Evaluator {
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
     (void)nfp;
-    auto kern = k_eval_fused<NB, H, D>;
+    auto kern = k_eval_fused<NB, H, D, Q>;
     static bool attr_set = false;
     if (!attr_set) {
       HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1603,24 +1692,26 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
   }
 
-  template <int NB, bool H>
+  template <int NB, bool H, bool Q>
   void dispatch_dens(int dens, int nfp, const double* dmu, double alpha, double* st, size_t nc) {
     switch (dens) {
-      case DENS_TANH: launch_fused<NB, H, DENS_TANH>(nfp, dmu, alpha, st, nc); break;
-      case DENS_EXP: launch_fused<NB, H, DENS_EXP>(nfp, dmu, alpha, st, nc); break;
-      case DENS_CUBE: launch_fused<NB, H, DENS_CUBE>(nfp, dmu, alpha, st, nc); break;
-      default: launch_fused<NB, H, DENS_LINEAR>(nfp, dmu, alpha, st, nc); break;
+      case DENS_TANH: launch_fused<NB, H, DENS_TANH, Q>(nfp, dmu, alpha, st, nc); break;
+      case DENS_EXP: launch_fused<NB, H, DENS_EXP, Q>(nfp, dmu, alpha, st, nc); break;
+      case DENS_CUBE: launch_fused<NB, H, DENS_CUBE, Q>(nfp, dmu, alpha, st, nc); break;
+      default: launch_fused<NB, H, DENS_LINEAR, false>(nfp, dmu, alpha, st, nc); break;  // Gram
     }
   }
+  // Σy² (Q) is accumulated with H (non-orthogonal) or when the caller asks for it
   template <int NB>
-  void dispatch_h(bool h, int dens, int nfp, const double* dmu, double alpha, double* st, size_t nc) {
+  void dispatch_h(bool h, bool q, int dens, int nfp, const double* dmu, double alpha, double* st, size_t nc) {
     if constexpr (NB == 8) {  // H at nc > 64 goes to the tiled path (register budget)
       if (h) throw computation_error("fused pass with H needs nc <= 64");
-      dispatch_dens<NB, false>(dens, nfp, dmu, alpha, st, nc);
-    } else {
-      if (h) dispatch_dens<NB, true>(dens, nfp, dmu, alpha, st, nc);
-      else dispatch_dens<NB, false>(dens, nfp, dmu, alpha, st, nc);
+    } else if (h) {
+      dispatch_dens<NB, true, true>(dens, nfp, dmu, alpha, st, nc);
+      return;
     }
+    if (q) dispatch_dens<NB, false, true>(dens, nfp, dmu, alpha, st, nc);
+    else dispatch_dens<NB, false, false>(dens, nfp, dmu, alpha, st, nc);
   }
 
   void run_eval(const double* w, size_t nc, const double* mu, int dens, double alpha, bool need_h, double* stats_host) {
@@ -1650,10 +1741,10 @@ struct DeviceCtx : Evaluator {
       ensure(d_w, cap_w, wp.size());
       HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
       switch (nb) {
-        case 1: dispatch_h<1>(need_h, dens, nfp, dmu, alpha, st, nc); break;
-        case 2: dispatch_h<2>(need_h, dens, nfp, dmu, alpha, st, nc); break;
-        case 4: dispatch_h<4>(need_h, dens, nfp, dmu, alpha, st, nc); break;
-        default: dispatch_h<8>(need_h, dens, nfp, dmu, alpha, st, nc); break;
+        case 1: dispatch_h<1>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+        case 2: dispatch_h<2>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+        case 4: dispatch_h<4>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+        default: dispatch_h<8>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
       }
     } else {
       generic_eval(w, nc, dmu, dens, alpha, need_h, st);
@@ -1878,7 +1969,7 @@ struct DeviceCtx : Evaluator {
     return true;
   }
 
-  template <int NB, int D>
+  template <int NB, int D, bool Q>
   void launch_loss(const double* dmu, double alpha, bool store, double* st_rows) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
@@ -1888,10 +1979,10 @@ struct DeviceCtx : Evaluator {
     const size_t lds = (size_t)2 * S::TS * 16 * NB * 16 * sizeof(double);
     HIP_OK(hipEventRecord(ev[1], stream));
     if (store) {
-      k_eval_loss<NB, D, true><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw,
+      k_eval_loss<NB, D, true, Q><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw,
                                                                     n_blocks, part, d_ybuf);
     } else {
-      k_eval_loss<NB, D, false><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha,
+      k_eval_loss<NB, D, false, Q><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha,
                                                                      bpw, n_blocks, part, nullptr);
     }
     HIP_OK(hipGetLastError());
@@ -2000,17 +2091,19 @@ struct DeviceCtx : Evaluator {
     ensure(d_w, cap_w, wp.size());
     HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
     kept_nc_pending = nc;
-#define PC_LOSS(NBV)                                                                            \
+#define PC_LOSS(NBV, Q)                                                                         \
   switch (d.kind) {                                                                             \
-    case DENS_TANH: launch_loss<NBV, DENS_TANH>(dmu, d.alpha, store, st_rows); break;            \
-    case DENS_EXP: launch_loss<NBV, DENS_EXP>(dmu, d.alpha, store, st_rows); break;              \
-    default: launch_loss<NBV, DENS_CUBE>(dmu, d.alpha, store, st_rows); break;                   \
+    case DENS_TANH: launch_loss<NBV, DENS_TANH, Q>(dmu, d.alpha, store, st_rows); break;         \
+    case DENS_EXP: launch_loss<NBV, DENS_EXP, Q>(dmu, d.alpha, store, st_rows); break;           \
+    default: launch_loss<NBV, DENS_CUBE, Q>(dmu, d.alpha, store, st_rows); break;                \
   }
+    // Σy² only where it is read (non-orthogonal: need_h) or asked for
+    const bool q = need_h || want_y2;
     switch (nb) {
-      case 1: PC_LOSS(1); break;
-      case 2: PC_LOSS(2); break;
-      case 4: PC_LOSS(4); break;
-      default: PC_LOSS(8); break;
+      case 1: if (q) { PC_LOSS(1, true); } else { PC_LOSS(1, false); } break;
+      case 2: if (q) { PC_LOSS(2, true); } else { PC_LOSS(2, false); } break;
+      case 4: if (q) { PC_LOSS(4, true); } else { PC_LOSS(4, false); } break;
+      default: if (q) { PC_LOSS(8, true); } else { PC_LOSS(8, false); } break;
     }
 #undef PC_LOSS
     allreduce(st_rows, 2 * nc);

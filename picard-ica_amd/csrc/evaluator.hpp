@@ -47,6 +47,10 @@ struct EvalStats {
 class Evaluator {
  public:
   virtual ~Evaluator() = default;
+  // Σy² (the last nc stats) is always computed with H; without H only if
+  // want_y2 (the orthogonal solver never reads it: core.rs:221 computes Y∘Y
+  // but only :274 and the extended non-orthogonal loss use it). Otherwise 0.
+  bool want_y2 = true;
   virtual uint64_t n_features() const = 0;
   virtual uint64_t n_samples() const = 0;  // global T over all ranks
   virtual void rowsum(double* out) = 0;

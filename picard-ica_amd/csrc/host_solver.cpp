@@ -215,6 +215,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
 
 void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
+  ev_->want_y2 = !cfg_.ortho;  // Σy² is read only by the non-orthogonal step / extended loss
   ev_->eval(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
   ++last_evals_;
   ++total_evals_;
@@ -222,6 +223,7 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
 
 bool Solver::evaluate_loss(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
+  ev_->want_y2 = !cfg_.ortho;
   const bool partial =
       ev_->eval_loss(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out, keep_y_);
   ++last_evals_;

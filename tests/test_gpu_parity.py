@@ -77,18 +77,36 @@ def test_eval_no_mean_and_tiny_t(pa, po, rng):
             assert rel_err(got[k], want[k]) <= TOL, (t, k)
 
 
+@pytest.mark.parametrize("n", [8, 64, 128])
+@pytest.mark.parametrize("dens", DENSITIES)
+def test_skip_y2_changes_nothing_else(pa, rng, n, dens):
+    """PC_EVAL_SKIP_Y2 (the orthogonal solver's mode): Σy² reads 0, every other
+    statistic is bit-identical to the pass that accumulates Σy²."""
+    x = laplace_mix(rng, n, 3001)
+    ctx = ctx_with(pa, x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = pa.DensityType(["tanh", "exp", "cube"].index(dens[0]), dens[1])
+    a = ctx.eval(w, mu, d, False, need_y2=True)
+    b = ctx.eval(w, mu, d, False, need_y2=False)
+    for k in ("G", "dpsi", "ll"):
+        assert np.array_equal(a[k], b[k]), k
+    if dens[0] != "cube":  # cube keeps Σy² (its Σψ′ = 3·Σy²)
+        assert not b["y2"].any()
+
+
 @pytest.mark.parametrize("n", [8, 30, 64, 128, 200])
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
-@pytest.mark.parametrize("need_h", [False, True])
-def test_split_eval_bit_identical(pa, rng, n, dens, need_h):
+@pytest.mark.parametrize("need_h,need_y2", [(False, True), (True, True), (False, False)])
+def test_split_eval_bit_identical(pa, rng, n, dens, need_h, need_y2):
     """Loss-only try + completion from the kept Y == one fused pass, bit for bit."""
     x = laplace_mix(rng, n, 4099)
     ctx = ctx_with(pa, x)
     w = rng.normal(size=(n, n)) / np.sqrt(n)
     mu = x.mean(axis=1)
     d = pa.DensityType(["tanh", "exp", "cube"].index(dens[0]), dens[1])
-    full = ctx.eval(w, mu, d, need_h)
-    loss_only, kept, done = ctx.eval_split(w, mu, d, need_h)
+    full = ctx.eval(w, mu, d, need_h, need_y2=need_y2)
+    loss_only, kept, done = ctx.eval_split(w, mu, d, need_h, need_y2=need_y2)
     assert np.array_equal(loss_only["ll"], full["ll"]) and np.array_equal(loss_only["y2"], full["y2"])
     if kept:
         assert np.isnan(loss_only["G"]).all()
