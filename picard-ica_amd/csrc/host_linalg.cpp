@@ -8,21 +8,85 @@
 
 namespace pcamd {
 
+// C = A·B for the small dense N×N products of the host driver (matrix_exp's
+// 30-term Taylor series is the biggest user: ~40 products of N×N per line-search
+// try). Register-blocked 4 rows × 32 columns with fma, every element summed over
+// p in increasing order (so any thread count gives the same bits, as the
+// lockstep multi-rank drivers require). Compiled for AVX-512 and AVX2 (both
+// with FMA) plus a plain fallback; the variant is picked once from cpuid.
+namespace {
+constexpr size_t MB = 4, NBW = 32;
+
+#define PC_MM_BLOCK_BODY                                                           \
+  double acc[MB][NBW] = {};                                                        \
+  for (size_t p = 0; p < k; ++p) {                                                 \
+    const double* bp = B + p * m + j0;                                             \
+    for (size_t r = 0; r < MB; ++r) {                                              \
+      const double a = A[(i0 + r) * k + p];                                       \
+      for (size_t j = 0; j < NBW; ++j) acc[r][j] = __builtin_fma(a, bp[j], acc[r][j]); \
+    }                                                                              \
+  }                                                                                \
+  for (size_t r = 0; r < MB; ++r)                                                  \
+    for (size_t j = 0; j < NBW; ++j) C[(i0 + r) * m + j0 + j] = acc[r][j];
+
+__attribute__((target("avx512f,avx512vl,fma"))) void mm_block_avx512(const double* A, const double* B, double* C,
+                                                                     size_t k, size_t m, size_t i0, size_t j0) {
+  PC_MM_BLOCK_BODY
+}
+__attribute__((target("avx2,fma"))) void mm_block_avx2(const double* A, const double* B, double* C, size_t k,
+                                                        size_t m, size_t i0, size_t j0) {
+  PC_MM_BLOCK_BODY
+}
+void mm_block_plain(const double* A, const double* B, double* C, size_t k, size_t m, size_t i0, size_t j0) {
+  PC_MM_BLOCK_BODY
+}
+#undef PC_MM_BLOCK_BODY
+
+using mm_block_fn = void (*)(const double*, const double*, double*, size_t, size_t, size_t, size_t);
+mm_block_fn pick_mm_block() {
+  __builtin_cpu_init();
+  if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("fma"))
+    return mm_block_avx512;
+  if (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) return mm_block_avx2;
+  return mm_block_plain;
+}
+const mm_block_fn mm_block = pick_mm_block();
+
+void mm_edge(const double* A, const double* B, double* C, size_t k, size_t m, size_t i0, size_t i1, size_t j0,
+             size_t j1) {
+  for (size_t i = i0; i < i1; ++i)
+    for (size_t j = j0; j < j1; ++j) {
+      double s = 0.0;
+      for (size_t p = 0; p < k; ++p) s += A[i * k + p] * B[p * m + j];
+      C[i * m + j] = s;
+    }
+}
+}  // namespace
+
 Mat matmul(const Mat& a, const Mat& b) {
   Mat c(a.rows, b.cols);
   const size_t n = a.rows, k = a.cols, m = b.cols;
   const double* A = a.data();
   const double* B = b.data();
   double* C = c.data();
-  // i-k-j order: contiguous inner loop over the output row; rows in parallel.
-#pragma omp parallel for schedule(static) if (n * k * m > (1u << 18))
-  for (long i = 0; i < (long)n; ++i) {
-    double* ci = C + (size_t)i * m;
-    for (size_t p = 0; p < k; ++p) {
-      const double aip = A[(size_t)i * k + p];
-      const double* bp = B + p * m;
-#pragma omp simd
-      for (size_t j = 0; j < m; ++j) ci[j] += aip * bp[j];
+  if (m < NBW) {  // tiny (C1-sized) products: plain i-k-j
+    for (size_t i = 0; i < n; ++i)
+      for (size_t p = 0; p < k; ++p) {
+        const double aip = A[i * k + p];
+        for (size_t j = 0; j < m; ++j) C[i * m + j] += aip * B[p * m + j];
+      }
+    return c;
+  }
+  const size_t nb = n / MB, mb = m / NBW;
+  const long tiles = (long)(nb * mb);
+#pragma omp parallel if (n * k * m > (1u << 20))
+  {
+#pragma omp for schedule(static) nowait
+    for (long t = 0; t < tiles; ++t) mm_block(A, B, C, k, m, (size_t)(t / mb) * MB, (size_t)(t % mb) * NBW);
+#pragma omp single nowait
+    {
+      if (mb * NBW < m) mm_edge(A, B, C, k, m, 0, nb * MB, mb * NBW, m);
+      if (nb * MB < n) mm_edge(A, B, C, k, m, nb * MB, n, 0, m);
     }
   }
   return c;

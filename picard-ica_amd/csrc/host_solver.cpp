@@ -6,11 +6,17 @@
 // Every N×T quantity comes from the Evaluator (one fused device pass).
 #include "host_solver.hpp"
 
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
+#include <mutex>
+#include <omp.h>
+#include <thread>
 
 namespace pcamd {
 
@@ -286,6 +292,48 @@ void Solver::init_core() {  // core.rs:175-209
   }
 }
 
+// Orthogonal line search, host side: W_k = expm(α_k·D)·W (core.rs:118-125) for
+// α_k = 2^-k. Try 0's map is on the critical path; a helper thread forms the
+// maps of tries 1, 2, … while the device evaluates the earlier tries, so the
+// N³ Taylor series (math.rs:38-74) is hidden behind the passes. Same operations
+// in the same order as the serial loop: identical bits.
+class TransformsAhead {
+ public:
+  TransformsAhead(const Mat& d, const Mat& w, size_t tries) : w_(tries), ready_(tries, 0) {
+    th_ = std::thread([this, d, w, tries] {
+      omp_set_num_threads(1);  // background work: leave the cores to the thread driving the device
+      double alpha = 1.0;
+      for (size_t k = 1; k < tries && !stop_.load(std::memory_order_relaxed); ++k) {
+        alpha /= 2.0;
+        Mat wk = matmul(matrix_exp(scale(d, alpha)), w);
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          w_[k] = std::move(wk);
+          ready_[k] = 1;
+        }
+        cv_.notify_all();
+      }
+    });
+  }
+  ~TransformsAhead() {
+    stop_ = true;
+    if (th_.joinable()) th_.join();
+  }
+  Mat get(size_t k) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return ready_[k] != 0; });
+    return w_[k];
+  }
+
+ private:
+  std::vector<Mat> w_;
+  std::vector<char> ready_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::atomic<bool> stop_{false};
+  std::thread th_;
+};
+
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first) {  // core.rs:99-150
   // Evaluation schedule: a try is a full fused pass, or a loss-only pass
   // completed (G, H, Σψ′) only if that try becomes the new iterate (both
@@ -296,15 +344,21 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
   LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false};
+  std::unique_ptr<TransformsAhead> ahead;
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
-      transform = matrix_exp(scale(direction, alpha));
+      if (k == 0) {
+        r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
+        if (tries > 1) ahead.reset(new TransformsAhead(direction, W_, tries));
+      } else {
+        r.w = ahead->get(k);
+      }
     } else {
       transform = Mat::eye(n);
       for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += alpha * direction.a[e];
+      r.w = matmul(transform, W_);
     }
-    r.w = matmul(transform, W_);
     if (!ortho && !no_multi_ && (k == 1 || (k == 0 && multi_first))) {
       // Non-ortho: Y_α = Y + α·Z is linear in α, so the remaining tries share
       // one pass (see eval_loss_multi); only the accepted try is evaluated in full.
