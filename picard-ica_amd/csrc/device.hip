@@ -1052,6 +1052,125 @@ k_tiled_y(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, 
   }
 }
 
+// Phase 1 with W in registers (nf ≤ 256): the workgroup pair-member
+// blockIdx.y = role owns output rows [128·role, 128·role + 128); wave w owns
+// row block ib = 8·role + w and keeps its W fragment (16 rows × NFP) in VGPRs
+// for the whole launch, so W is read once — the LDS-chunked k_tiled_y re-read
+// all of W from L2 for every 64-sample tile (4× the X traffic at N = 256).
+// X̃ blocks of 16 samples × NFP features are staged through LDS (shared by the
+// 8 waves; double-buffered, prefetch pinned one block ahead) and Yᵀ tiles come
+// from ONE chain of KS MFMAs per wave, as in k_eval_fused. Row terms use the
+// mask-free RowAcc (raw sums, finalized in k_reduce_tiled).
+template <int KS, int DENS, int MODE>  // MODE 0: y, ψ (, ψ′) fragments + all row terms; 1: Σℓ, Σy² terms only
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, int ncp,
+           const double* __restrict__ WpT, const double* __restrict__ mu, double alpha, uint64_t bpw,
+           uint64_t n_blocks, double* __restrict__ partials, int accumulate, double* __restrict__ ybuf,
+           double* __restrict__ pbuf, double* __restrict__ dbuf) {
+  constexpr int NFP = 4 * KS, XS = 16 * NFP, PRE = XS / 2 / FUSED_THREADS;
+  static_assert(XS / 2 % FUSED_THREADS == 0, "X block must split evenly over the workgroup");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  const int ib = blockIdx.y * 8 + wave;
+  const bool active = ib < nib;
+  const int row = ib * 16 + lr;
+  const double alpha_ = alpha, inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
+  extern __shared__ double smem[];
+  double* xs0 = smem;  // [2][NFP][16]
+  double wf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) wf[ks] = active ? WpT[(size_t)(4 * ks + lk) * ncp + row] : 0.0;
+  RowAcc racc;
+  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint64_t b_last = b_end - 1;
+  int xk[PRE], xt[PRE];
+  double xmu[PRE];
+  const double* xsrc[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) {
+    const int e = tid + p * FUSED_THREADS;
+    xk[p] = e / 8;
+    xt[p] = 2 * (e % 8);
+    const bool ok = xk[p] < nf;
+    xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
+    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
+  }
+  double2 pre[PRE];
+  auto load_x = [&](uint64_t b) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * 16);
+  };
+  auto store_x = [&](uint64_t b, double* xs) {
+    if (b * 16 + 16 <= n_in) {
+#pragma unroll
+      for (int p = 0; p < PRE; ++p)
+        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
+    } else {
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        const uint64_t tg = b * 16 + xt[p];
+        double2 v;
+        v.x = tg < n_in ? pre[p].x - xmu[p] : 0.0;
+        v.y = tg + 1 < n_in ? pre[p].y - xmu[p] : 0.0;
+        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = v;
+      }
+    }
+  };
+  // blocks past n_in (the rest of the last 64-sample tile) are loaded clamped and
+  // staged as zeros: their y = ψ = 0 fragments add nothing in phase 2
+  auto clampb = [&](uint64_t b) { return b * 16 < n_in ? b : (n_in ? (n_in - 1) / 16 : 0); };
+  if (b_begin < b_end) {
+    load_x(clampb(b_begin));
+    store_x(b_begin, xs0);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      load_x(clampb(b < b_last ? b + 1 : b_last));
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) {
+        d4 yv = d4{0, 0, 0, 0};
+        const double* xrow = xs0 + cur * XS + lk * 16 + lr;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
+        if constexpr (MODE == 0) {
+          double psi[4], dpsi[4];
+          density_acc4<DENS, true, true, 1>(yv, alpha_, m2a, racc, psi, dpsi);
+          const uint64_t tt = b >> 2;
+          const int ts = (int)(b & 3);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const size_t f = tl_frag(tt, ib, ts, r, nib) + lane;
+            ybuf[f] = yv[r];
+            pbuf[f] = psi[r];
+            if (dbuf) dbuf[f] = dpsi[r];
+          }
+        } else {
+          loss_acc4<DENS, true, 1>(yv, alpha_, m2a, racc);
+        }
+        if (b & 1) acc_renorm<DENS>(racc);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      store_x(b < b_last ? b + 1 : b_last, xs0 + (cur ^ 1) * XS);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  // raw row terms → workgroup partials [Σψ′ | Σℓ | Σy²] (ncp each); the two
+  // roles of a slot write disjoint rows
+  double rs_d = acc_dpsi<DENS>(racc), rs_l = acc_ll<DENS>(racc, inv_alpha), rs_q = racc.q;
+  rs_d += __shfl_xor(rs_d, 16); rs_d += __shfl_xor(rs_d, 32);
+  rs_l += __shfl_xor(rs_l, 16); rs_l += __shfl_xor(rs_l, 32);
+  rs_q += __shfl_xor(rs_q, 16); rs_q += __shfl_xor(rs_q, 32);
+  if (active && lk == 0) {
+    double* out = partials + (size_t)blockIdx.x * 3 * ncp;
+    const double v[3] = {MODE == 0 ? rs_d : 0.0, rs_l, rs_q};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[c * ncp + row] = accumulate ? out[c * ncp + row] + v[c] : v[c];
+  }
+}
+
 // G_raw (, H_raw) tiles of 128×128 from the phase-1 fragments; blockIdx.x = tile, blockIdx.y = T split.
 template <bool NEED_H>
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
@@ -1245,8 +1364,10 @@ k_multi_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 
 
 // stats[e] for the tiled path: G/H from slabs (sum over splits), rows from phase-1 partials.
+// Row terms from k_tiled_yw are raw (finalize_row with dens ≥ 0); k_tiled_y's are final (dens < 0).
 __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, const double* __restrict__ rows,
-                               int nwg1, int ncp, int nc, bool need_h, int rows_only, double* __restrict__ stats) {
+                               int nwg1, int ncp, int nc, bool need_h, int rows_only, double* __restrict__ stats,
+                               int dens, double alpha, double n) {
   const size_t nsq = (size_t)nc * nc, psq = (size_t)ncp * ncp;
   const size_t mats = rows_only ? 0 : (need_h ? 2 : 1) * nsq;
   const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -1263,7 +1384,7 @@ __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, con
     if (rows_only && c == 0) return;  // loss-only: Σψ′ not computed
     double s = 0.0;
     for (int w = 0; w < nwg1; ++w) s += rows[(size_t)w * 3 * ncp + c * ncp + row];
-    stats[base_rows + f] = s;
+    stats[base_rows + f] = dens < 0 ? s : finalize_row(dens, alpha, n, (int)c, s);
   }
 }
 
@@ -1836,6 +1957,33 @@ struct DeviceCtx : Evaluator {
   static bool tiled_ok(size_t nc, int dens, double alpha) {
     return nc <= 256 && !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0)) && dens <= DENS_LINEAR;
   }
+  // register-W phase 1 (k_tiled_yw) for nf ≤ 256: K steps per MFMA chain, 0 = use k_tiled_y
+  static int yw_ks(uint64_t nf) { return nf <= 64 ? 16 : nf <= 128 ? 32 : nf <= 256 ? 64 : 0; }
+  template <int KS, int D>
+  void yw_launch_ks(int mode, int ncp, const double* dmu, double alpha, uint64_t ntl, int nwg1, bool acc,
+                    const double* X0, uint64_t n_in, double* yb, double* pb, double* db) {
+    const uint64_t n_blocks = ntl * 4;  // whole 64-sample tiles: phase 2 reads every sub-block
+    const uint64_t bpw = (n_blocks + nwg1 - 1) / nwg1;
+    const int nroles = (ncp / 16 + 7) / 8;
+    const size_t lds = (size_t)2 * 16 * 4 * KS * sizeof(double);
+    auto k = mode == 0 ? k_tiled_yw<KS, D, 0> : k_tiled_yw<KS, D, 1>;
+    static bool attr[2] = {false, false};
+    if (!attr[mode]) {
+      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr[mode] = true;
+    }
+    k<<<dim3(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, n_in, (int)nf, ncp, d_w, dmu, alpha, bpw,
+                                                          n_blocks, d_trow, acc ? 1 : 0, yb, pb, db);
+  }
+  template <int D>
+  void yw_launch(int mode, int ncp, const double* dmu, double alpha, uint64_t ntl, int nwg1, bool acc,
+                 const double* X0, uint64_t n_in, double* yb, double* pb, double* db) {
+    switch (yw_ks(nf)) {
+      case 16: yw_launch_ks<16, D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in, yb, pb, db); break;
+      case 32: yw_launch_ks<32, D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in, yb, pb, db); break;
+      default: yw_launch_ks<64, D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in, yb, pb, db); break;
+    }
+  }
   template <int D>
   void tiled_launch(int mode, int nfp, int ncp, const double* dmu, double alpha, uint64_t tile0, uint64_t ntl,
                     bool need_h, int nsplit, int nwg1, uint64_t tpw, bool acc, const double* X0) {
@@ -1852,8 +2000,12 @@ struct DeviceCtx : Evaluator {
       attr[mode] = true;
     }
     const uint64_t n_in_chunk = std::min<uint64_t>(n_local_ - tile0 * TL_TT, ntl * TL_TT);
-    k1<<<nwg1, FUSED_THREADS, lds, stream>>>(X0, ldx, n_in_chunk, (int)nf, nfp, ncp, d_w, dmu, alpha, tpw, ntl,
-                                             d_trow, acc ? 1 : 0, yb, pb, db);
+    if (yw_ks(nf)) {
+      yw_launch<D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in_chunk, yb, pb, db);
+    } else {
+      k1<<<nwg1, FUSED_THREADS, lds, stream>>>(X0, ldx, n_in_chunk, (int)nf, nfp, ncp, d_w, dmu, alpha, tpw, ntl,
+                                               d_trow, acc ? 1 : 0, yb, pb, db);
+    }
     HIP_OK(hipGetLastError());
     if (mode == 0) {
       const int nto = (ncp / 16 + 7) / 8;
@@ -1869,7 +2021,8 @@ struct DeviceCtx : Evaluator {
   void tiled_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st,
                   int mode) {
     const int ncp = (int)((nc + 31) / 32 * 32);
-    const int nfp = (int)((nf + TL_KC - 1) / TL_KC * TL_KC);
+    const int ks = yw_ks(nf);
+    const int nfp = ks ? 4 * ks : (int)((nf + TL_KC - 1) / TL_KC * TL_KC);  // k_tiled_yw reads 4·KS rows
     std::vector<double> wt((size_t)nfp * ncp, 0.0);  // Wᵀ, zero-padded
     for (size_t i = 0; i < nc; ++i)
       for (size_t k = 0; k < nf; ++k) wt[k * ncp + i] = w[i * nf + k];
@@ -1879,7 +2032,9 @@ struct DeviceCtx : Evaluator {
     // T chunks bound the fragment buffers to ~24 GB (3 arrays of ncp × chunk)
     const uint64_t max_tiles = std::max<uint64_t>(1, (uint64_t)(24e9 / (3.0 * ncp * TL_TT * sizeof(double))));
     const uint64_t ct = std::min<uint64_t>(n_tiles, max_tiles);
-    const int nwg1 = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(ct, 1));
+    const int nwg1 = ks ? (int)std::min<uint64_t>((uint64_t)n_cu * 2 / ((ncp / 16 + 7) / 8),
+                                                  std::max<uint64_t>(ct * 4, 1))
+                        : (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(ct, 1));
     const int nto = (ncp / 16 + 7) / 8;
     const int nsplit = (int)std::max<uint64_t>(1, std::min<uint64_t>(ct, (uint64_t)(2 * n_cu / (nto * nto))));
     if (mode == 0) {
@@ -1902,7 +2057,8 @@ struct DeviceCtx : Evaluator {
     }
     const size_t total = (size_t)(mode == 0 ? (need_h ? 2 : 1) * nc * nc : 0) + 3 * nc;
     k_reduce_tiled<<<(total + 255) / 256, 256, 0, stream>>>(d_slab, nsplit, d_trow, nwg1, ncp, (int)nc, need_h,
-                                                            mode == 1 ? 1 : 0, st);
+                                                            mode == 1 ? 1 : 0, st, ks ? dens : -1, alpha,
+                                                            (double)n_local_);
     HIP_OK(hipGetLastError());
   }
 
