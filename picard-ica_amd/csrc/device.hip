@@ -1171,6 +1171,113 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   }
 }
 
+// Phase 2 staged through LDS: blockIdx.x = 128×128 output tile (ti, tj),
+// blockIdx.y = T split. Per 16-sample sub-block the workgroup copies the ψ
+// (and ψ′) fragments of its 8 row blocks ti and the y fragments of row blocks
+// tj (16 KB each, contiguous 2 KB runs) into LDS once — every fragment feeds 2
+// or 4 waves — with the next sub-block prefetched into registers a full
+// iteration ahead; one barrier per sub-block. Wave (gi, gj) accumulates a 64×32
+// patch of G (and H) in registers.
+template <bool NEED_H>
+__global__ void __launch_bounds__(FUSED_THREADS, 1)
+k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, const double* __restrict__ dbuf,
+              int ncp, uint64_t n_tiles, uint64_t tps, double* __restrict__ slabs, int accumulate) {
+  constexpr int NARR = NEED_H ? 3 : 2;  // staged arrays: ψ, y (, ψ′)
+  constexpr int SUB = 8 * 256;          // doubles per array per sub-block (8 row blocks × 4 r × 64)
+  constexpr int PRE = NARR * SUB / 2 / FUSED_THREADS;  // 2 slots per array
+  static_assert(SUB == 4 * FUSED_THREADS, "slot map assumes 512 threads");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  const int nto = (nib + 7) / 8;
+  const int ti = blockIdx.x / nto, tj = blockIdx.x % nto;
+  const int gi0 = (wave >> 2) * 4, gj0 = (wave & 3) * 2;  // local row blocks
+  extern __shared__ double smem[];
+  double* lds = smem;  // [2][NARR][8][4][64]
+  d4 accg[4][2], acch[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
+  // staging slots: slot p of thread tid is double e = 2·tid + 1024·p of the
+  // [NARR][8][256] sub-block image, i.e. array p/2 (ψ, y, ψ′), local row block
+  // tid/128 + 4·(p&1), offset 2·tid mod 256 — all slots share one in-array offset
+  const int lb0 = tid >> 7, off = (2 * tid) & 255;
+  int soff[PRE];
+  bool ok[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) {
+    const int gb = ((p >> 1) == 1 ? tj : ti) * 8 + lb0 + 4 * (p & 1);  // y uses the tj row blocks
+    ok[p] = gb < nib;
+    soff[p] = (ok[p] ? gb : 0) * 1024 + off;  // + ((tt·nib)·4 + ts)·256 per sub-block
+  }
+  const uint64_t t_begin = (uint64_t)blockIdx.y * tps;
+  const uint64_t t_end = t_begin + tps < n_tiles ? t_begin + tps : n_tiles;
+  const uint64_t s_begin = t_begin * 4, s_end = t_end * 4;  // sub-blocks
+  double2 pre[PRE];
+  auto load = [&](uint64_t sb) {
+    const size_t o = ((sb >> 2) * (size_t)nib * 4 + (sb & 3)) * 256;
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      const double* base = (p >> 1) == 0 ? pbuf : (p >> 1) == 1 ? ybuf : dbuf;
+      pre[p] = ok[p] ? *reinterpret_cast<const double2*>(base + o + soff[p]) : double2{0.0, 0.0};
+    }
+  };
+  auto store = [&](double* img) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) *reinterpret_cast<double2*>(img + 2 * tid + 1024 * p) = pre[p];
+  };
+  if (s_begin < s_end) {
+    load(s_begin);
+    store(lds);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t sb = s_begin; sb < s_end; ++sb) {
+      load(sb + 1 < s_end ? sb + 1 : sb);
+      __builtin_amdgcn_sched_barrier(0);
+      const double* img = lds + cur * NARR * SUB;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double pa[4], da[4], yb[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pa[i] = img[((gi0 + i) * 4 + r) * 64 + lane];
+          if constexpr (NEED_H) da[i] = img[2 * SUB + ((gi0 + i) * 4 + r) * 64 + lane];
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) yb[j] = img[SUB + ((gj0 + j) * 4 + r) * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            accg[i][j] = mfma(pa[i], yb[j], accg[i][j]);
+            if constexpr (NEED_H) acch[i][j] = mfma(da[i], yb[j] * yb[j], acch[i][j]);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      store(lds + (cur ^ 1) * NARR * SUB);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  const size_t nsq = (size_t)ncp * ncp;
+  double* slab = slabs + (size_t)blockIdx.y * (NEED_H ? 2 : 1) * nsq;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int bi = ti * 8 + gi0 + i, bj = tj * 8 + gj0 + j;
+      if (bi < nib && bj < nib)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = bi * 16 + lk + 4 * r, col = bj * 16 + lr;
+          const size_t o = (size_t)row * ncp + col;
+          slab[o] = accumulate ? slab[o] + accg[i][j][r] : accg[i][j][r];
+          if constexpr (NEED_H) slab[nsq + o] = accumulate ? slab[nsq + o] + acch[i][j][r] : acch[i][j][r];
+        }
+    }
+}
+
 // G_raw (, H_raw) tiles of 128×128 from the phase-1 fragments; blockIdx.x = tile, blockIdx.y = T split.
 template <bool NEED_H>
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
@@ -2010,10 +2117,21 @@ struct DeviceCtx : Evaluator {
     if (mode == 0) {
       const int nto = (ncp / 16 + 7) / 8;
       const uint64_t tps = (ntl + nsplit - 1) / nsplit;
-      if (need_h)
-        k_tiled_gram<true><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
-      else
-        k_tiled_gram<false><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      if (std::getenv("PICARD_GRAM_V1")) {  // experiment knob: the unstaged phase 2
+        if (need_h)
+          k_tiled_gram<true><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+        else
+          k_tiled_gram<false><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      } else {
+        const size_t lds2 = (size_t)2 * (need_h ? 3 : 2) * 8 * 256 * sizeof(double);
+        static bool attr2[2] = {false, false};
+        auto k2 = need_h ? k_tiled_gram2<true> : k_tiled_gram2<false>;
+        if (!attr2[need_h]) {
+          HIP_OK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+          attr2[need_h] = true;
+        }
+        k2<<<dim3(nto * nto, nsplit), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      }
       HIP_OK(hipGetLastError());
     }
   }
