@@ -905,7 +905,8 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
 }
 
 // out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets (fixed order)
-// then finalize_row(dens, α, n, c0 + c, ·) unless dens < 0 (already final)
+// then finalize_row(dens, α, n, c0 + c, ·) unless dens < 0 (already final);
+// c0 < 0: the sets alternate [Σℓ, Σy²] per try (multi-try layout)
 __global__ void k_reduce_rows(const double* __restrict__ partials, int nwg, size_t pstride, size_t poff, int ncp,
                               int nc, int nsets, double* __restrict__ out, int dens, double alpha, double n, int c0) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -913,7 +914,7 @@ __global__ void k_reduce_rows(const double* __restrict__ partials, int nwg, size
   const int c = e / nc, row = e % nc;
   double s = 0.0;
   for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + poff + (size_t)c * ncp + row];
-  out[e] = dens < 0 ? s : finalize_row(dens, alpha, n, c0 + c, s);
+  out[e] = dens < 0 ? s : finalize_row(dens, alpha, n, c0 < 0 ? 1 + (c & 1) : c0 + c, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1470,6 +1471,151 @@ k_multi_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 }
 
 
+// Multi-try loss pass with W and Z = D·W in registers (nf ≤ 256). A workgroup
+// covers 64 rows (blockIdx.y = role: row blocks 4·role … 4·role+3); wave w owns
+// row block w&3 and the K-half w>>2, holding the matching halves of its W and Z
+// fragments (2 × NFP/8 doubles per lane), so neither matrix is re-read per tile
+// (k_multi_loss re-staged both from L2 for every 32-sample tile). Per 16-sample
+// block: partial Yᵀ and Zᵀ tiles from two single MFMA chains over the K-half,
+// exchanged through LDS (double-buffered, one barrier per block) and summed in
+// K order; then each wave of the pair evaluates every other try α_j on
+// y = Y + α_j·Z with the mask-free RowAcc terms (finalized in k_reduce_rows).
+constexpr int ML2_TRIES = (ML_NA + 1) / 2;  // tries per wave
+template <int KS, int DENS, bool NEED_Q>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int ncp,
+              const double* __restrict__ WpT, const double* __restrict__ ZpT, const double* __restrict__ mu,
+              double alpha, const double* __restrict__ alphas, int na, uint64_t bpw, uint64_t n_blocks,
+              double* __restrict__ partials) {
+  constexpr int NFP = 4 * KS, KH = KS / 2, XS = 16 * NFP, PRE = XS / 2 / FUSED_THREADS;
+  static_assert(XS / 2 % FUSED_THREADS == 0, "X block must split evenly over the workgroup");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  const int rb = wave & 3, kh = wave >> 2;
+  const int ib = blockIdx.y * 4 + rb;
+  const bool active = ib < nib;
+  const int row = ib * 16 + lr;
+  const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
+  extern __shared__ double smem[];
+  double* xs0 = smem;             // [2][NFP][16]
+  double* ex0 = smem + 2 * XS;    // [2][2 K-halves][4 row blocks][Y, Z][4][64]
+  double wf[KH], zf[KH];
+#pragma unroll
+  for (int q = 0; q < KH; ++q) {
+    const size_t o = (size_t)(4 * (kh * KH + q) + lk) * ncp + row;
+    wf[q] = active ? WpT[o] : 0.0;
+    zf[q] = active ? ZpT[o] : 0.0;
+  }
+  // this wave's tries: j = kh, kh + 2, … < na
+  double aj[ML2_TRIES];
+  RowAcc racc[ML2_TRIES];
+#pragma unroll
+  for (int u = 0; u < ML2_TRIES; ++u) aj[u] = (kh + 2 * u < na) ? alphas[kh + 2 * u] : 0.0;
+  const int my_na = na > kh ? (na - kh + 1) / 2 : 0;
+  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint64_t b_last = b_end - 1;
+  int xk[PRE], xt[PRE];
+  double xmu[PRE];
+  const double* xsrc[PRE];
+#pragma unroll
+  for (int p = 0; p < PRE; ++p) {
+    const int e = tid + p * FUSED_THREADS;
+    xk[p] = e / 8;
+    xt[p] = 2 * (e % 8);
+    const bool ok = xk[p] < nf;
+    xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
+    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
+  }
+  double2 pre[PRE];
+  auto load_x = [&](uint64_t b) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * 16);
+  };
+  auto store_x = [&](uint64_t b, double* xs) {
+    if (b * 16 + 16 <= n_local) {
+#pragma unroll
+      for (int p = 0; p < PRE; ++p)
+        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
+    } else {
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        const uint64_t tg = b * 16 + xt[p];
+        double2 v;
+        v.x = tg < n_local ? pre[p].x - xmu[p] : 0.0;
+        v.y = tg + 1 < n_local ? pre[p].y - xmu[p] : 0.0;
+        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = v;
+      }
+    }
+  };
+  auto exch = [&](int buf, int half, int yz, int r) -> double* {
+    return ex0 + ((((buf * 2 + half) * 4 + rb) * 2 + yz) * 4 + r) * 64 + lane;
+  };
+  if (b_begin < b_end) {
+    load_x(b_begin);
+    store_x(b_begin, xs0);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      load_x(b < b_last ? b + 1 : b_last);
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) {  // partial Yᵀ, Zᵀ over this wave's K-half
+        d4 ya = d4{0, 0, 0, 0}, za = d4{0, 0, 0, 0};
+        const double* xrow = xs0 + cur * XS + (4 * kh * KH + lk) * 16 + lr;
+#pragma unroll
+        for (int q = 0; q < KH; ++q) {
+          const double xa = xrow[(4 * q) * 16];
+          ya = mfma(xa, wf[q], ya);
+          za = mfma(xa, zf[q], za);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          *exch(cur, kh, 0, r) = ya[r];
+          *exch(cur, kh, 1, r) = za[r];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      store_x(b < b_last ? b + 1 : b_last, xs0 + (cur ^ 1) * XS);
+      __syncthreads();
+      if (active) {  // Y, Z summed in K order (identical in both waves of the pair), then the tries
+        d4 yv, zv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          yv[r] = *exch(cur, 0, 0, r) + *exch(cur, 1, 0, r);
+          zv[r] = *exch(cur, 0, 1, r) + *exch(cur, 1, 1, r);
+        }
+#pragma unroll
+        for (int u = 0; u < ML2_TRIES; ++u) {
+          if (u < my_na) {
+            d4 yj;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj[u], zv[r], yv[r]);
+            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, racc[u]);
+            if (b & 1) acc_renorm<DENS>(racc[u]);
+          }
+        }
+      }
+      cur ^= 1;
+    }
+  }
+  // partials: [ML_NA][2][ncp] raw (Σℓ term, Σy²) per try
+  double* out = partials + (size_t)blockIdx.x * ML_NA * 2 * ncp;
+#pragma unroll
+  for (int u = 0; u < ML2_TRIES; ++u) {
+    if (u < my_na) {
+      double l = acc_ll<DENS>(racc[u], inv_alpha), q = racc[u].q;
+      l += __shfl_xor(l, 16); l += __shfl_xor(l, 32);
+      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+      if (active && lk == 0) {
+        const int j = kh + 2 * u;
+        out[(j * 2 + 0) * ncp + row] = l;
+        out[(j * 2 + 1) * ncp + row] = q;
+      }
+    }
+  }
+}
+
 // stats[e] for the tiled path: G/H from slabs (sum over splits), rows from phase-1 partials.
 // Row terms from k_tiled_yw are raw (finalize_row with dens ≥ 0); k_tiled_y's are final (dens < 0).
 __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, const double* __restrict__ rows,
@@ -1634,22 +1780,35 @@ __global__ void k_sum_slabs(const double* __restrict__ slabs, int splits, size_t
 }
 
 // Row sums Σ_t X[k][t] over this shard: partials[wg][k], T split over workgroups.
-__global__ void k_rowsum(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, uint64_t per,
-                         double* __restrict__ partials) {
+__global__ void __launch_bounds__(256) k_rowsum(const double* __restrict__ X, uint64_t ldx, uint64_t n_local,
+                                                int nf, uint64_t per, double* __restrict__ partials) {
+  // blockIdx.y = row k, blockIdx.x = slice [t0, t0 + per) of the (zero-padded) row;
+  // 16-B loads, four independent partial sums per thread for memory-level parallelism
   __shared__ double red[256];
-  const uint64_t t0 = blockIdx.x * per, t1 = std::min<uint64_t>(n_local, t0 + per);
-  for (int k = 0; k < nf; ++k) {
-    double s = 0.0;
-    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) s += X[(size_t)k * ldx + t];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
+  const int k = blockIdx.y;
+  const uint64_t t0 = blockIdx.x * per, t1 = std::min<uint64_t>(ldx, t0 + per);
+  const double* row = X + (size_t)k * ldx;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  uint64_t t = t0 + 2 * threadIdx.x;
+  for (; t + 3 * 512 < t1; t += 4 * 512) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double2 v = *reinterpret_cast<const double2*>(row + t + u * 512);
+      s[u] += v.x + v.y;
     }
-    if (threadIdx.x == 0) partials[(size_t)blockIdx.x * nf + k] = red[0];
+  }
+  for (; t < t1; t += 512) {
+    const double2 v = *reinterpret_cast<const double2*>(row + t);
+    s[0] += v.x + v.y;
+  }
+  red[threadIdx.x] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
+  if (threadIdx.x == 0) partials[(size_t)blockIdx.x * nf + k] = red[0];
+  (void)n_local;  // columns past n_local are zero (alloc_x zero-fills the padding)
 }
 
 // Fourth moments for JADE: out[p][q] += Σ_t z_p z_q, z_(i≤j) = y_i y_j, over a Y chunk.
@@ -1854,11 +2013,14 @@ struct DeviceCtx : Evaluator {
 
   void rowsum(double* out) override {
     HIP_OK(hipSetDevice(device));
-    const int nwg = n_cu;
-    const uint64_t per = (n_local_ + nwg - 1) / nwg;
+    // ≥ 8 workgroups per CU in total, slices a multiple of 512 samples (16-B loads)
+    const uint64_t slices = std::max<uint64_t>(1, std::min<uint64_t>((ldx + 511) / 512,
+                                                                     (uint64_t)(8 * n_cu + nf - 1) / nf));
+    const uint64_t per = ((ldx + slices - 1) / slices + 511) / 512 * 512;
+    const int nwg = (int)((ldx + per - 1) / per);
     double* part = ensure(d_part, cap_part, (size_t)nwg * nf);
     double* st = ensure(d_stats, cap_stats, nf);
-    k_rowsum<<<nwg, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, per, part);
+    k_rowsum<<<dim3(nwg, (unsigned)nf), 256, 0, stream>>>(X, ldx, n_local_, (int)nf, per, part);
     HIP_OK(hipGetLastError());
     k_sum_slabs<<<(nf + 255) / 256, 256, 0, stream>>>(part, nwg, nf, st);
     allreduce(st, nf);
@@ -1993,11 +2155,36 @@ struct DeviceCtx : Evaluator {
 
   // ---- non-ortho multi-try loss pass ---------------------------------------
   // ll_out / y2_out: [na][nc] (Σℓ, Σy² of Y + α_j·Z), summed over ranks
+  template <int KS, int D>
+  void multi2_launch(int ncp, const double* dw, const double* dz, const double* dmu, double alpha,
+                     const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks, double* part) {
+    const int nroles = (ncp / 16 + 3) / 4;
+    const size_t lds = (size_t)(2 * 16 * 4 * KS + 2 * 2 * 4 * 2 * 4 * 64) * sizeof(double);
+    auto k = want_y2 ? k_multi_loss2<KS, D, true> : k_multi_loss2<KS, D, false>;
+    static bool attr[2] = {false, false};
+    if (!attr[want_y2]) {
+      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr[want_y2] = true;
+    }
+    k<<<dim3(nwg, nroles), FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, ncp, dw, dz, dmu, alpha, dal, na,
+                                                         bpw, n_blocks, part);
+  }
+  template <int D>
+  void multi2_dispatch(int ks, int ncp, const double* dw, const double* dz, const double* dmu, double alpha,
+                       const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks, double* part) {
+    switch (ks) {
+      case 16: multi2_launch<16, D>(ncp, dw, dz, dmu, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      case 32: multi2_launch<32, D>(ncp, dw, dz, dmu, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      default: multi2_launch<64, D>(ncp, dw, dz, dmu, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+    }
+  }
+
   void multi_loss(const double* w, const double* z, size_t nc, const double* mu, pc_density d, const double* alphas,
                   int na, double* ll_out, double* y2_out) {
     HIP_OK(hipSetDevice(device));
     const int ncp = (int)((nc + 31) / 32 * 32);
-    const int nfp = (int)((nf + ML_KC - 1) / ML_KC * ML_KC);
+    const int ks = std::getenv("PICARD_MULTI_V1") ? 0 : yw_ks(nf);  // register-resident k_multi_loss2
+    const int nfp = ks ? 4 * ks : (int)((nf + ML_KC - 1) / ML_KC * ML_KC);
     std::vector<double> wt((size_t)2 * nfp * ncp + ML_NA, 0.0);
     for (size_t i = 0; i < nc; ++i)
       for (size_t k = 0; k < nf; ++k) {
@@ -2013,14 +2200,35 @@ struct DeviceCtx : Evaluator {
       dmu = ensure(d_mu, cap_mu, nf);
       HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
     }
+    const size_t pst = (size_t)ML_NA * 2 * ncp;
+    const double* dal = dw + (size_t)2 * nfp * ncp;
+    if (ks) {
+      const uint64_t n_blocks = std::max<uint64_t>((n_local_ + 15) / 16, 1);
+      const int nroles = (ncp / 16 + 3) / 4;
+      const int nwg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)2 * n_cu / nroles, n_blocks));
+      const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
+      double* part = ensure(d_part, cap_part, (size_t)nwg * pst);
+      HIP_OK(hipEventRecord(ev[1], stream));
+      switch (d.kind) {
+        case DENS_TANH: multi2_dispatch<DENS_TANH>(ks, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+        case DENS_EXP: multi2_dispatch<DENS_EXP>(ks, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+        default: multi2_dispatch<DENS_CUBE>(ks, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      }
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipEventRecord(ev[2], stream));
+      double* st = ensure(d_stats, cap_stats, (size_t)2 * na * nc);
+      k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
+                                                                          d.kind, d.alpha, (double)n_local_, -1);
+      HIP_OK(hipGetLastError());
+      multi_finish(st, nc, na, ll_out, y2_out);
+      return;
+    }
     const uint64_t n_tiles = (n_local_ + ML_TT - 1) / ML_TT;
     const int nwg = (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(n_tiles, 1));
     const uint64_t tpw = (std::max<uint64_t>(n_tiles, 1) + nwg - 1) / nwg;
-    const size_t pst = (size_t)ML_NA * 2 * ncp;
     double* part = ensure(d_part, cap_part, (size_t)nwg * pst);
     HIP_OK(hipMemsetAsync(part, 0, (size_t)nwg * pst * sizeof(double), stream));
     const size_t lds = (size_t)(2 * ML_KC * (256 + 16) + ML_KC * (ML_TT + 16) + 8 * ML_NA * 2 * 16 * 2) * sizeof(double);
-    const double* dal = dw + (size_t)2 * nfp * ncp;
     HIP_OK(hipEventRecord(ev[1], stream));
     switch (d.kind) {
       case DENS_TANH: k_multi_loss<DENS_TANH><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, nfp, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, tpw, n_tiles, part); break;
@@ -2034,6 +2242,9 @@ struct DeviceCtx : Evaluator {
     k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
                                                                         -1, 0.0, 0.0, 0);
     HIP_OK(hipGetLastError());
+    multi_finish(st, nc, na, ll_out, y2_out);
+  }
+  void multi_finish(double* st, size_t nc, int na, double* ll_out, double* y2_out) {
     allreduce(st, (size_t)2 * na * nc);
     std::vector<double> h((size_t)2 * na * nc);
     HIP_OK(hipMemcpyAsync(h.data(), st, h.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
