@@ -7,6 +7,7 @@
 #include "host_solver.hpp"
 
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -624,7 +625,9 @@ Mat Solver::jade(size_t max_iter, double tol) {
   const size_t np = n * (n + 1) / 2;
   std::vector<double> m4(np * np);
   Mat base = has_k_ ? K_ : Mat::eye(nf_);
+  const auto tj0 = std::chrono::steady_clock::now();
   ev_->moments4(base.data(), n, has_mu_ ? mu_.data() : nullptr, m4.data());
+  const auto tj1 = std::chrono::steady_clock::now();
   std::vector<size_t> pidx(n * n);
   {
     size_t q = 0;
@@ -632,70 +635,136 @@ Mat Solver::jade(size_t max_iter, double tol) {
       for (size_t j = i; j < n; ++j) { pidx[i * n + j] = pidx[j * n + i] = q++; }
   }
   const double t = (double)T_;
-  std::vector<Mat> R;  // rotated cumulant matrices, in jade.rs's (i ≤ j) order
-  R.reserve(np);
-  for (size_t i = 0; i < n; ++i)
-    for (size_t j = i; j < n; ++j) {
-      Mat q(n, n);
-      const size_t pij = pidx[i * n + j];
-      for (size_t k = 0; k < n; ++k)
-        for (size_t l = 0; l < n; ++l) {
-          double e = m4[pij * np + pidx[k * n + l]] / t;
+  // Cumulant matrices Q_ij (jade.rs:101-126), symmetrised, stored packed by
+  // position: A[pos(k,l)][m] for k ≤ l, matrix index m innermost, so a Givens
+  // step on (p, q) streams 2n contiguous rows of length np and the g-sums of
+  // jade.rs:137-167 are three contiguous dot products.
+  auto pos = [n](size_t k, size_t l) {  // k ≤ l
+    return k * n - k * (k - 1) / 2 + (l - k);
+  };
+  const size_t npos = n * (n + 1) / 2;
+  std::vector<double> A(npos * np);
+  {
+    size_t m = 0;
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = i; j < n; ++j, ++m) {
+        const size_t pij = pidx[i * n + j];
+        auto q = [&](size_t k, size_t l) {
+          const double e = m4[pij * np + pidx[k * n + l]] / t;
           const double d1 = (i == j && k == l) ? 1.0 : 0.0;
           const double d2 = (i == k && j == l) ? 1.0 : 0.0;
           const double d3 = (i == l && j == k) ? 1.0 : 0.0;
-          q(k, l) = e - d1 - d2 - d3;
-        }
-      Mat qs(n, n);
-      for (size_t k = 0; k < n; ++k)
-        for (size_t l = 0; l < n; ++l) qs(k, l) = (q(k, l) + q(l, k)) / 2.0;
-      R.push_back(std::move(qs));
-    }
+          return e - d1 - d2 - d3;
+        };
+        for (size_t k = 0; k < n; ++k)
+          for (size_t l = k; l < n; ++l) A[pos(k, l) * np + m] = (q(k, l) + q(l, k)) / 2.0;
+      }
+  }
   if (cfg_.verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
   Mat v = Mat::eye(n);
-  for (size_t it = 0; it < max_iter; ++it) {
-    double max_theta = 0.0;
-    for (size_t p = 0; p < n; ++p)
-      for (size_t q = p + 1; q < n; ++q) {
+  // Sweeps in the reference's cyclic (p, q) order. The np matrices are split
+  // into NCH fixed chunks; each thread rotates its chunks and forms their
+  // partial g-sums for the NEXT pair, and every thread sums the partials in
+  // chunk order to the same angle — one barrier per pair, results independent
+  // of the thread count.
+  constexpr size_t NCH = 64;
+  const size_t nch = std::min<size_t>(NCH, np);
+  std::vector<double> gpart(2 * nch * 3, 0.0);
+  std::vector<std::pair<size_t, size_t>> pairs;
+  for (size_t p = 0; p < n; ++p)
+    for (size_t q = p + 1; q < n; ++q) pairs.emplace_back(p, q);
+  auto chunk_lo = [&](size_t c) { return c * np / nch; };
+  auto partial_g = [&](size_t p, size_t q, size_t c, double* g) {
+    const double* apq = A.data() + pos(p, q) * np;
+    const double* app = A.data() + pos(p, p) * np;
+    const double* aqq = A.data() + pos(q, q) * np;
+    double g00 = 0, g01 = 0, g11 = 0;
+    for (size_t m = chunk_lo(c); m < chunk_lo(c + 1); ++m) {
+      const double h_pq = apq[m] + apq[m];  // M(p,q) + M(q,p)
+      const double h_pp_qq = app[m] - aqq[m];
+      g00 += h_pq * h_pq;
+      g01 += h_pq * h_pp_qq;
+      g11 += h_pp_qq * h_pp_qq;
+    }
+    g[0] = g00; g[1] = g01; g[2] = g11;
+  };
+  size_t sweeps_done = 0;
+  bool converged = false;
+#pragma omp parallel
+  {
+    const int nt = omp_get_num_threads(), tid = omp_get_thread_num();
+    const size_t c0 = nch * tid / nt, c1 = nch * (tid + 1) / nt;
+    int buf = 0;
+    for (size_t c = c0; c < c1; ++c) partial_g(pairs[0].first, pairs[0].second, c, &gpart[(0 * nch + c) * 3]);
+#pragma omp barrier
+    for (size_t it = 0; it < max_iter && !converged; ++it) {
+      double max_theta = 0.0;
+      for (size_t pi = 0; pi < pairs.size(); ++pi) {
+        const size_t p = pairs[pi].first, q = pairs[pi].second;
         double g00 = 0, g01 = 0, g11 = 0;
-        for (const Mat& m : R) {
-          const double h_pq = m(p, q) + m(q, p);
-          const double h_pp_qq = m(p, p) - m(q, q);
-          g00 += h_pq * h_pq;
-          g01 += h_pq * h_pp_qq;
-          g11 += h_pp_qq * h_pp_qq;
+        for (size_t c = 0; c < nch; ++c) {
+          const double* g = &gpart[(buf * nch + c) * 3];
+          g00 += g[0]; g01 += g[1]; g11 += g[2];
         }
         const double diff = g11 - g00;
         const double angle = (std::fabs(g01) < 1e-15 && std::fabs(diff) < 1e-15) ? 0.0 : 0.25 * std::atan2(2.0 * g01, diff);
-        const double c = std::cos(angle), s = std::sin(angle);
+        const double cs = std::cos(angle), sn = std::sin(angle);
         max_theta = std::fmax(max_theta, std::fabs(angle));
-        for (size_t i = 0; i < n; ++i) {  // jade.rs:188-197
-          const double vp = v(i, p), vq = v(i, q);
-          v(i, p) = c * vp - s * vq;
-          v(i, q) = s * vp + c * vq;
+        if (tid == 0)
+          for (size_t i = 0; i < n; ++i) {  // jade.rs:188-197
+            const double vp = v(i, p), vq = v(i, q);
+            v(i, p) = cs * vp - sn * vq;
+            v(i, q) = sn * vp + cs * vq;
+          }
+        // A ← Gᵀ A G on this thread's chunks: rows/columns p, q of every matrix
+        for (size_t c = c0; c < c1; ++c) {
+          const size_t m0 = chunk_lo(c), m1 = chunk_lo(c + 1);
+          for (size_t k = 0; k < n; ++k) {
+            if (k == p || k == q) continue;
+            double* ap = A.data() + (k < p ? pos(k, p) : pos(p, k)) * np;
+            double* aq = A.data() + (k < q ? pos(k, q) : pos(q, k)) * np;
+            for (size_t m = m0; m < m1; ++m) {
+              const double mp = ap[m], mq = aq[m];
+              ap[m] = cs * mp - sn * mq;
+              aq[m] = sn * mp + cs * mq;
+            }
+          }
+          double* app = A.data() + pos(p, p) * np;
+          double* apq = A.data() + pos(p, q) * np;
+          double* aqq = A.data() + pos(q, q) * np;
+          for (size_t m = m0; m < m1; ++m) {  // the 2×2 block: columns, then rows
+            const double a = app[m], b = apq[m], d = aqq[m];
+            const double pp = cs * a - sn * b, pq = sn * a + cs * b;  // row p after M·G
+            const double qp = cs * b - sn * d, qq = sn * b + cs * d;  // row q after M·G
+            app[m] = cs * pp - sn * qp;
+            apq[m] = cs * pq - sn * qq;
+            aqq[m] = sn * pq + cs * qq;
+          }
+          if (pi + 1 < pairs.size())
+            partial_g(pairs[pi + 1].first, pairs[pi + 1].second, c, &gpart[((buf ^ 1) * nch + c) * 3]);
+          else
+            partial_g(pairs[0].first, pairs[0].second, c, &gpart[((buf ^ 1) * nch + c) * 3]);
         }
-        // R ← Gᵀ R G with G the same rotation of columns p, q
-#pragma omp parallel for schedule(static)
-        for (long mi = 0; mi < (long)R.size(); ++mi) {
-          Mat& m = R[mi];
-          for (size_t k = 0; k < n; ++k) {
-            const double mp = m(k, p), mq = m(k, q);
-            m(k, p) = c * mp - s * mq;
-            m(k, q) = s * mp + c * mq;
-          }
-          for (size_t k = 0; k < n; ++k) {
-            const double mp = m(p, k), mq = m(q, k);
-            m(p, k) = c * mp - s * mq;
-            m(q, k) = s * mp + c * mq;
-          }
+        buf ^= 1;
+#pragma omp barrier
+      }
+      if (tid == 0) {
+        sweeps_done = it + 1;
+        if (cfg_.verbose && (it + 1) % 10 == 0)
+          std::printf("JADE iteration %zu: max angle = %s\n", it + 1, rust_e4(max_theta).c_str());
+        if (max_theta < tol) {
+          if (cfg_.verbose) std::printf("JADE converged after %zu iterations\n", it + 1);
+          converged = true;
         }
       }
-    if (cfg_.verbose && (it + 1) % 10 == 0)
-      std::printf("JADE iteration %zu: max angle = %s\n", it + 1, rust_e4(max_theta).c_str());
-    if (max_theta < tol) {
-      if (cfg_.verbose) std::printf("JADE converged after %zu iterations\n", it + 1);
-      break;
+#pragma omp barrier
     }
+  }
+  (void)sweeps_done;
+  if (std::getenv("PICARD_TRACE")) {
+    const auto tj2 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[picard-trace] jade: moments %.3f s, sweeps %.3f s\n",
+                 std::chrono::duration<double>(tj1 - tj0).count(), std::chrono::duration<double>(tj2 - tj1).count());
   }
   Mat w;
   if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
