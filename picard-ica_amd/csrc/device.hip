@@ -1846,6 +1846,96 @@ __global__ void __launch_bounds__(256) k_moments4(const double* __restrict__ Y, 
     }
 }
 
+// Fourth moments for JADE on MFMA (jade.rs:91-113 as a Gram of pair products):
+// M4[p][q] = Σ_t z_p z_q, z_(i≤j) = y_i y_j. blockIdx.x = upper-triangle 128×128
+// output tile (tp ≤ tq), blockIdx.y = T split. Per 16-sample sub-block the Y
+// rows are staged in LDS, each thread forms 8 pair products straight into the
+// MFMA A/B fragment layout in LDS (every product feeds 2 or 4 waves), and wave
+// (gi, gj) accumulates a 64×32 patch; one barrier per sub-block. Slab s holds
+// split s's partial tile (summed in fixed order by k_moments4_reduce).
+__global__ void __launch_bounds__(FUSED_THREADS, 1)
+k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc, const int* __restrict__ pi,
+                const int* __restrict__ pj, int np, const int* __restrict__ tile_p, const int* __restrict__ tile_q,
+                uint64_t spb, double* __restrict__ slabs, size_t slab_stride) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int tp = tile_p[blockIdx.x], tq = tile_q[blockIdx.x];
+  const int gi0 = (wave >> 2) * 4, gj0 = (wave & 3) * 2;
+  extern __shared__ double smem[];
+  double* ys = smem;              // [nc][16] Y sub-block
+  double* zf = smem + 64 * 16;    // [2 (P, Q)][8 pair blocks][4 k-steps][64 lanes]
+  d4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0, 0, 0, 0};
+  // this thread's 8 products per sub-block: element e = tid + 512·u of the
+  // [2][8][4][64] fragment image → pair (set, block, lane&15), sample 4·kk + lane>>4
+  int ia[8], ja[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + FUSED_THREADS * u;
+    const int set = e >> 11, blk = (e >> 8) & 7, ln = e & 63;
+    const int pr = (set ? tq : tp) * 128 + blk * 16 + (ln & 15);
+    ia[u] = pr < np ? pi[pr] : -1;
+    ja[u] = pr < np ? pj[pr] : -1;
+  }
+  const uint64_t nsb = (cn + 15) / 16;
+  const uint64_t s_begin = blockIdx.y * spb, s_end = s_begin + spb < nsb ? s_begin + spb : nsb;
+  for (uint64_t sb = s_begin; sb < s_end; ++sb) {
+    for (int e = tid; e < nc * 16; e += FUSED_THREADS) {
+      const int r = e >> 4, c = e & 15;
+      const uint64_t t = sb * 16 + c;
+      ys[e] = t < cn ? Y[(size_t)r * ldy + t] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + FUSED_THREADS * u;
+      const int kk = (e >> 6) & 3, ln = e & 63;
+      const int t = 4 * kk + (ln >> 4);
+      zf[e] = ia[u] >= 0 ? ys[ia[u] * 16 + t] * ys[ja[u] * 16 + t] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      double a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = zf[((gi0 + i) * 4 + kk) * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = zf[2048 + ((gj0 + j) * 4 + kk) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  double* out = slabs + blockIdx.y * slab_stride;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = tp * 128 + (gi0 + i) * 16 + lk + 4 * r, q = tq * 128 + (gj0 + j) * 16 + lr;
+        if (p < np && q < np) out[(size_t)p * np + q] = acc[i][j][r];
+      }
+  (void)lr;
+}
+
+// acc[p][q] (+)= Σ_s slabs[s][p][q] for the upper tiles written by k_moments4_mfma
+__global__ void k_moments4_reduce(const double* __restrict__ slabs, int nsplit, size_t slab_stride, int np,
+                                  int accumulate, double* __restrict__ acc) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= (size_t)np * np) return;
+  const int p = (int)(e / np), q = (int)(e % np);
+  if (q / 128 < p / 128) return;  // lower tiles: not computed (mirrored on the host)
+  double s = 0.0;
+  for (int k = 0; k < nsplit; ++k) s += slabs[k * slab_stride + e];
+  acc[e] = accumulate ? acc[e] + s : s;
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic mixture (benches/benchmarks.rs:8-35), generated in HBM.
 // S[i][t] from LCG state number i·T + t + 1 (jump-ahead per column, then the
@@ -2703,22 +2793,50 @@ struct DeviceCtx : Evaluator {
       dmu = ensure(d_mu, cap_mu, nf);
       HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
     }
-    const uint64_t CH = 1ull << 16;
-    const size_t need = nc * CH + (size_t)np * np + 2 * (size_t)np;
+    const bool mfma_path = nc <= 64 && std::getenv("PICARD_MOMENTS_V1") == nullptr;
+    const uint64_t CH = mfma_path ? (1ull << 22) : (1ull << 16);
+    // tiles of the upper triangle and the T split (≈ whole rounds of one workgroup per CU)
+    const int nt = (np + 127) / 128;
+    std::vector<int> tpv, tqv;
+    for (int a = 0; a < nt; ++a)
+      for (int b = a; b < nt; ++b) { tpv.push_back(a); tqv.push_back(b); }
+    const int ntile = (int)tpv.size();
+    const int nsplit = mfma_path ? std::max(1, (int)std::lround(3.0 * n_cu / ntile)) : 1;
+    const size_t slab_stride = (size_t)np * np;
+    const size_t need = nc * CH + (size_t)np * np + 2 * (size_t)np + 2 * (size_t)ntile +
+                        (mfma_path ? nsplit * slab_stride : 0);
     double* Y = ensure(d_chunk, cap_chunk, need);
     double* acc = Y + nc * CH;
     int* dpi = reinterpret_cast<int*>(acc + (size_t)np * np);
     int* dpj = dpi + np;
+    int* dtp = dpj + np;
+    int* dtq = dtp + ntile;
+    double* slabs = acc + (size_t)np * np + 2 * (size_t)np + 2 * (size_t)ntile;  // int arrays sized in doubles
     HIP_OK(hipMemcpyAsync(dpi, pi.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dpj, pj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dtp, tpv.data(), ntile * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dtq, tqv.data(), ntile * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemsetAsync(acc, 0, (size_t)np * np * sizeof(double), stream));
     const int tiles = (np + 31) / 32;
+    bool first = true;
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
       const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
       k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, 0.0, c0,
                                                                cn, Y, CH, nullptr, nullptr, nullptr, 0);
-      k_moments4<<<tiles * tiles, 256, 0, stream>>>(Y, CH, cn, (int)nc, dpi, dpj, np, acc);
+      if (mfma_path) {
+        const uint64_t nsb = (cn + 15) / 16;
+        const uint64_t spb = (nsb + nsplit - 1) / nsplit;
+        const size_t lds = (size_t)(64 * 16 + 2 * 8 * 4 * 64) * sizeof(double);
+        k_moments4_mfma<<<dim3(ntile, nsplit), FUSED_THREADS, lds, stream>>>(Y, CH, cn, (int)nc, dpi, dpj, np, dtp, dtq,
+                                                                            spb, slabs, slab_stride);
+        HIP_OK(hipGetLastError());
+        k_moments4_reduce<<<(unsigned)(((size_t)np * np + 255) / 256), 256, 0, stream>>>(slabs, nsplit, slab_stride, np,
+                                                                                         first ? 0 : 1, acc);
+      } else {
+        k_moments4<<<tiles * tiles, 256, 0, stream>>>(Y, CH, cn, (int)nc, dpi, dpj, np, acc);
+      }
       HIP_OK(hipGetLastError());
+      first = false;
     }
     allreduce(acc, (size_t)np * np);
     HIP_OK(hipMemcpyAsync(out, acc, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, stream));
@@ -2726,6 +2844,7 @@ struct DeviceCtx : Evaluator {
     for (int p = 0; p < np; ++p)  // mirror the upper tiles
       for (int q = 0; q < p; ++q) out[(size_t)p * np + q] = out[(size_t)q * np + p];
   }
+
 };
 
 // factory + thin accessors used by capi.cpp
