@@ -904,17 +904,36 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
   }
 }
 
-// out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets (fixed order)
+// Fixed-order sum of per-workgroup partials, shared by every reduction of the
+// register-resident kernels so their common statistics stay bit-identical: a
+// 256-thread block reduces 64 outputs, each as 4 contiguous groups of workgroups
+// summed in order, then ((g0 + g1) + (g2 + g3)).
+constexpr int RED_OUT = 64;
+__device__ __forceinline__ double reduce_partials(const double* __restrict__ p, int nwg, size_t pstride, bool ok,
+                                                  double (*red)[RED_OUT]) {
+  const int g = threadIdx.x / RED_OUT, o = threadIdx.x % RED_OUT;
+  double s = 0.0;
+  if (ok)
+    for (int w = nwg * g / 4; w < nwg * (g + 1) / 4; ++w) s += p[(size_t)w * pstride];
+  red[g][o] = s;
+  __syncthreads();
+  return (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
+}
+
+// out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets,
 // then finalize_row(dens, α, n, c0 + c, ·) unless dens < 0 (already final);
 // c0 < 0: the sets alternate [Σℓ, Σy²] per try (multi-try layout)
-__global__ void k_reduce_rows(const double* __restrict__ partials, int nwg, size_t pstride, size_t poff, int ncp,
-                              int nc, int nsets, double* __restrict__ out, int dens, double alpha, double n, int c0) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nsets * nc) return;
-  const int c = e / nc, row = e % nc;
-  double s = 0.0;
-  for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + poff + (size_t)c * ncp + row];
-  out[e] = dens < 0 ? s : finalize_row(dens, alpha, n, c0 < 0 ? 1 + (c & 1) : c0 + c, s);
+__global__ void __launch_bounds__(256) k_reduce_rows(const double* __restrict__ partials, int nwg, size_t pstride,
+                                                     size_t poff, int ncp, int nc, int nsets,
+                                                     double* __restrict__ out, int dens, double alpha, double n,
+                                                     int c0) {
+  __shared__ double red[4][RED_OUT];
+  const int e = blockIdx.x * RED_OUT + threadIdx.x % RED_OUT;
+  const bool ok = e < nsets * nc;
+  const int c = ok ? e / nc : 0, row = ok ? e % nc : 0;
+  const double s = reduce_partials(partials + poff + (size_t)c * ncp + row, nwg, pstride, ok, red);
+  if (ok && threadIdx.x < RED_OUT)
+    out[e] = dens < 0 ? s : finalize_row(dens, alpha, n, c0 < 0 ? 1 + (c & 1) : c0 + c, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1641,25 +1660,27 @@ __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, con
   }
 }
 
-// Fixed-order sum of per-workgroup partials into the compact stats layout
-// [G nc×nc | H nc×nc | Σψ′ nc | Σℓ nc | Σy² nc].
-__global__ void k_reduce(const double* __restrict__ partials, int nwg, size_t pstride, int ncp, int nc,
-                         bool need_h, double* __restrict__ stats, int dens, double alpha, double n) {
+// Per-workgroup partials into the compact stats layout
+// [G nc×nc | H nc×nc | Σψ′ nc | Σℓ nc | Σy² nc] (same order as k_reduce_rows).
+__global__ void __launch_bounds__(256) k_reduce(const double* __restrict__ partials, int nwg, size_t pstride,
+                                                int ncp, int nc, bool need_h, double* __restrict__ stats, int dens,
+                                                double alpha, double n) {
+  __shared__ double red[4][RED_OUT];
   const size_t nsq = (size_t)nc * nc;
   const size_t total = (need_h ? 2 : 1) * nsq + 3 * (size_t)nc;
-  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (e >= total) return;
-  size_t src;
-  if (e < nsq) src = (e / nc) * ncp + e % nc;
+  const size_t e = blockIdx.x * (size_t)RED_OUT + threadIdx.x % RED_OUT;
+  const bool ok = e < total;
+  size_t src = 0;
+  if (!ok) src = 0;
+  else if (e < nsq) src = (e / nc) * ncp + e % nc;
   else if (need_h && e < 2 * nsq) { const size_t f = e - nsq; src = (size_t)ncp * ncp + (f / nc) * ncp + f % nc; }
   else {
     const size_t f = e - (need_h ? 2 : 1) * nsq;
     src = (size_t)(need_h ? 2 : 1) * ncp * ncp + (f / nc) * ncp + f % nc;
   }
-  double s = 0.0;
-  for (int w = 0; w < nwg; ++w) s += partials[(size_t)w * pstride + src];
+  const double s = reduce_partials(partials + src, nwg, pstride, ok, red);
   const size_t mats = (need_h ? 2 : 1) * nsq;
-  stats[e] = e < mats ? s : finalize_row(dens, alpha, n, (int)((e - mats) / nc), s);
+  if (ok && threadIdx.x < RED_OUT) stats[e] = e < mats ? s : finalize_row(dens, alpha, n, (int)((e - mats) / nc), s);
 }
 
 // ---------------------------------------------------------------------------
@@ -2167,7 +2188,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t total = EvalStats::size(nc, H);
-    k_reduce<<<(total + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
+    k_reduce<<<(total + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
                                                       (double)n_local_);
     HIP_OK(hipGetLastError());
   }
@@ -2307,7 +2328,7 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(ev[2], stream));
       double* st = ensure(d_stats, cap_stats, (size_t)2 * na * nc);
-      k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
+      k_reduce_rows<<<(2 * na * (int)nc + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
                                                                           d.kind, d.alpha, (double)n_local_, -1);
       HIP_OK(hipGetLastError());
       multi_finish(st, nc, na, ll_out, y2_out);
@@ -2329,7 +2350,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventRecord(ev[2], stream));
     double* st = ensure(d_stats, cap_stats, (size_t)2 * na * nc);
     // st[(j·2 + c)·nc + row] = Σ_w part[w][(j·2 + c)·ncp + row]
-    k_reduce_rows<<<(2 * na * (int)nc + 255) / 256, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
+    k_reduce_rows<<<(2 * na * (int)nc + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pst, 0, ncp, (int)nc, 2 * na, st,
                                                                         -1, 0.0, 0.0, 0);
     HIP_OK(hipGetLastError());
     multi_finish(st, nc, na, ll_out, y2_out);
@@ -2562,7 +2583,8 @@ struct DeviceCtx : Evaluator {
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
-    k_reduce_rows<<<1, 512, 0, stream>>>(part, nwg, 2 * S::NCP, 0, S::NCP, (int)kept_nc_pending, 2, st_rows, D, alpha,
+    k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
+        part, nwg, 2 * S::NCP, 0, S::NCP, (int)kept_nc_pending, 2, st_rows, D, alpha,
                                          (double)n_local_, 1);
     HIP_OK(hipGetLastError());
   }
@@ -2583,7 +2605,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t nc = kept_nc;
     const size_t e1 = (H ? 2 : 1) * nc * nc + nc;  // [G | H | Σψ′]
-    k_reduce<<<(e1 + 255) / 256, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
+    k_reduce<<<(e1 + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
                                                    (double)n_local_);
     HIP_OK(hipGetLastError());
   }
