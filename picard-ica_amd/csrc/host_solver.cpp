@@ -300,42 +300,79 @@ void Solver::init_core() {  // core.rs:175-209
 // maps of tries 1, 2, … while the device evaluates the earlier tries, so the
 // N³ Taylor series (math.rs:38-74) is hidden behind the passes. Same operations
 // in the same order as the serial loop: identical bits.
-class TransformsAhead {
+// One persistent helper per solver. A search submits (D, W, tries) under a new
+// generation number; the helper forms its maps in order and drops a job as soon
+// as a newer one arrives. A finished search never waits for it (a stale
+// matrix_exp just completes in the background), which a per-search thread that
+// is joined at the end would do: up to one N³ series per iteration.
+class TransformWorker {
  public:
-  TransformsAhead(const Mat& d, const Mat& w, size_t tries) : w_(tries), ready_(tries, 0) {
-    th_ = std::thread([this, d, w, tries] {
-      omp_set_num_threads(1);  // background work: leave the cores to the thread driving the device
-      double alpha = 1.0;
-      for (size_t k = 1; k < tries && !stop_.load(std::memory_order_relaxed); ++k) {
-        alpha /= 2.0;
-        Mat wk = matmul(matrix_exp(scale(d, alpha)), w);
-        {
-          std::lock_guard<std::mutex> lk(mu_);
-          w_[k] = std::move(wk);
-          ready_[k] = 1;
-        }
-        cv_.notify_all();
-      }
-    });
+  TransformWorker() {
+    th_ = std::thread([this] { run(); });
   }
-  ~TransformsAhead() {
-    stop_ = true;
-    if (th_.joinable()) th_.join();
+  ~TransformWorker() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void submit(const Mat& d, const Mat& w, size_t tries) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++gen_;
+      d_ = d;
+      w_ = w;
+      tries_ = tries;
+      out_.assign(tries, Mat());
+      ready_.assign(tries, 0);
+    }
+    cv_.notify_all();
   }
   Mat get(size_t k) {
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] { return ready_[k] != 0; });
-    return w_[k];
+    return out_[k];
   }
 
  private:
-  std::vector<Mat> w_;
-  std::vector<char> ready_;
+  void run() {
+    omp_set_num_threads(1);  // background work: leave the cores to the thread driving the device
+    uint64_t done_gen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != done_gen; });
+      if (stop_) return;
+      const uint64_t g = gen_;
+      const Mat d = d_, w = w_;
+      const size_t tries = tries_;
+      double alpha = 1.0;
+      for (size_t k = 1; k < tries; ++k) {
+        alpha /= 2.0;
+        lk.unlock();
+        Mat wk = matmul(matrix_exp(scale(d, alpha)), w);
+        lk.lock();
+        if (stop_ || gen_ != g) break;  // superseded: drop the rest of this job
+        out_[k] = std::move(wk);
+        ready_[k] = 1;
+        cv_.notify_all();
+      }
+      done_gen = g;
+    }
+  }
+  std::thread th_;
   std::mutex mu_;
   std::condition_variable cv_;
-  std::atomic<bool> stop_{false};
-  std::thread th_;
+  bool stop_ = false;
+  uint64_t gen_ = 0;
+  Mat d_, w_;
+  size_t tries_ = 0;
+  std::vector<Mat> out_;
+  std::vector<char> ready_;
 };
+
+Solver::~Solver() = default;
 
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first) {  // core.rs:99-150
   // Evaluation schedule: a try is a full fused pass, or a loss-only pass
@@ -347,15 +384,17 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
   LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false};
-  std::unique_ptr<TransformsAhead> ahead;
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
       if (k == 0) {
         r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
-        if (tries > 1) ahead.reset(new TransformsAhead(direction, W_, tries));
+        if (tries > 1) {
+          if (!ahead_) ahead_.reset(new TransformWorker());
+          ahead_->submit(direction, W_, tries);
+        }
       } else {
-        r.w = ahead->get(k);
+        r.w = ahead_->get(k);
       }
     } else {
       transform = Mat::eye(n);

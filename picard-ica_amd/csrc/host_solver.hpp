@@ -2,6 +2,7 @@
 // src/lbfgs.rs:84-171 + src/jade.rs:22-197 restated over an Evaluator.
 #pragma once
 #include <deque>
+#include <memory>
 #include <random>
 
 #include "evaluator.hpp"
@@ -23,9 +24,12 @@ Mat compute_direction(const Mat& g, const Mat& h, const std::vector<double>& h_o
 Mat solve_hessian_system(const Mat& h, const std::vector<double>& h_off, const Mat& g);  // 136-150
 void regularize_hessian(Mat& h, const std::vector<double>& h_off, double lambda_min);   // 155-171
 
+class TransformWorker;  // host_solver.cpp: line-search maps formed ahead on a helper thread
+
 class Solver {
  public:
   Solver(Evaluator* ev, const pc_config& cfg);
+  ~Solver();
   // one iteration of core.rs:211-391; returns true once finished
   bool step();
   void finish(pc_result* out);
@@ -37,6 +41,7 @@ class Solver {
   uint64_t total_completions() const { return total_completions_; }
 
  private:
+  std::unique_ptr<TransformWorker> ahead_;
   double loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular);
   void evaluate(const Mat& w_core, EvalStats* out);
   bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
