@@ -336,3 +336,19 @@ def test_large_t_shard_additivity(pa, rng):
         assert rel_err(parts[0][k] + parts[1][k], full[k]) <= 1e-11, k
     # ortho Picard gradient at the true unmixing is small; at a random W it is not
     assert np.isfinite(full["G"]).all() and np.isfinite(full["ll"]).all()
+
+
+@pytest.mark.parametrize("n,t", [(64, 100_000), (128, 100_000)])
+def test_fit_c2_c3_shapes_vs_oracle(pa, po, dg, n, t):
+    """BASELINE configs 2 and 3 (Picard-O extended tanh at N = 64 / 128) at a T the
+    oracle fits in seconds: the register-resident fused / loss-only / split schedule
+    end to end against core::run. Both converge; Amari distance within 1e-6
+    (north_star); unmixing within 1e-6 relative; signs identical."""
+    x, s, a = dg.generate_data(n, t, 42)
+    r, ro = _fit_both(pa, po, x, max_iter=200)
+    assert r.converged and ro.converged
+    assert r.gradient_norm < 1e-7
+    am, amo = pa.utils.amari_distance(r.full_unmixing(), a), po.amari_distance(ro.full_unmixing(), a)
+    assert abs(am - amo) <= 1e-6
+    assert np.max(np.abs(r.full_unmixing() - ro.full_unmixing())) <= 1e-6 * np.max(np.abs(ro.full_unmixing()))
+    assert np.array_equal(r.signs, ro.signs)
