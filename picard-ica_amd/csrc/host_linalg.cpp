@@ -61,7 +61,68 @@ void mm_edge(const double* A, const double* B, double* C, size_t k, size_t m, si
       C[i * m + j] = s;
     }
 }
+// ---- JADE sweep kernels (host_solver.cpp: Solver::jade), same dispatch ----
+#define PC_GIVENS_BODY                                   \
+  for (size_t m = 0; m < len; ++m) {                     \
+    const double x = a[m], y = b[m];                     \
+    a[m] = c * x - s * y;                                \
+    b[m] = s * x + c * y;                                \
+  }
+__attribute__((target("avx512f,avx512vl"))) void givens_avx512(double* a, double* b, size_t len, double c, double s) {
+  PC_GIVENS_BODY
+}
+__attribute__((target("avx2"))) void givens_avx2(double* a, double* b, size_t len, double c, double s) {
+  PC_GIVENS_BODY
+}
+void givens_plain(double* a, double* b, size_t len, double c, double s) { PC_GIVENS_BODY }
+#undef PC_GIVENS_BODY
+
+// g-sums over 8 fixed lanes (m mod 8), combined in a fixed order: the same
+// value whichever instruction set runs it
+#define PC_GSUM_BODY                                                          \
+  double s00[8] = {}, s01[8] = {}, s11[8] = {};                              \
+  size_t m = 0;                                                               \
+  for (; m + 8 <= len; m += 8)                                                \
+    for (int j = 0; j < 8; ++j) {                                             \
+      const double hpq = apq[m + j] + apq[m + j], hd = app[m + j] - aqq[m + j]; \
+      s00[j] += hpq * hpq;                                                    \
+      s01[j] += hpq * hd;                                                     \
+      s11[j] += hd * hd;                                                      \
+    }                                                                         \
+  for (int j = 0; m < len; ++m, ++j) {                                        \
+    const double hpq = apq[m] + apq[m], hd = app[m] - aqq[m];                 \
+    s00[j] += hpq * hpq;                                                      \
+    s01[j] += hpq * hd;                                                       \
+    s11[j] += hd * hd;                                                        \
+  }                                                                           \
+  g[0] = ((s00[0] + s00[1]) + (s00[2] + s00[3])) + ((s00[4] + s00[5]) + (s00[6] + s00[7])); \
+  g[1] = ((s01[0] + s01[1]) + (s01[2] + s01[3])) + ((s01[4] + s01[5]) + (s01[6] + s01[7])); \
+  g[2] = ((s11[0] + s11[1]) + (s11[2] + s11[3])) + ((s11[4] + s11[5]) + (s11[6] + s11[7]));
+__attribute__((target("avx512f,avx512vl"))) void gsum_avx512(const double* apq, const double* app,
+                                                             const double* aqq, size_t len, double* g) {
+  PC_GSUM_BODY
+}
+__attribute__((target("avx2"))) void gsum_avx2(const double* apq, const double* app, const double* aqq, size_t len,
+                                              double* g) {
+  PC_GSUM_BODY
+}
+void gsum_plain(const double* apq, const double* app, const double* aqq, size_t len, double* g) { PC_GSUM_BODY }
+#undef PC_GSUM_BODY
+
+using givens_fn = void (*)(double*, double*, size_t, double, double);
+using gsum_fn = void (*)(const double*, const double*, const double*, size_t, double*);
+const givens_fn givens_impl = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl")
+                                  ? givens_avx512
+                                  : __builtin_cpu_supports("avx2") ? givens_avx2 : givens_plain;
+const gsum_fn gsum_impl = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl")
+                              ? gsum_avx512
+                              : __builtin_cpu_supports("avx2") ? gsum_avx2 : gsum_plain;
 }  // namespace
+
+void givens_rows(double* a, double* b, size_t len, double c, double s) { givens_impl(a, b, len, c, s); }
+void jade_gsums(const double* apq, const double* app, const double* aqq, size_t len, double* g) {
+  gsum_impl(apq, app, aqq, len, g);
+}
 
 Mat matmul(const Mat& a, const Mat& b) {
   Mat c(a.rows, b.cols);

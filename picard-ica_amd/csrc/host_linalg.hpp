@@ -45,6 +45,10 @@ Mat matrix_exp(const Mat& a);
 void sln_det(const Mat& m, double* sign, double* logabs);
 // math.rs:91-93
 Mat skew_symmetric(const Mat& a);
+// JADE sweep kernels: a ← c·a − s·b, b ← s·a + c·b elementwise; and the
+// g-sums of jade.rs:137-167 (Σ h_pq², Σ h_pq·h_d, Σ h_d², h_pq = 2·apq, h_d = app − aqq)
+void givens_rows(double* a, double* b, size_t len, double c, double s);
+void jade_gsums(const double* apq, const double* app, const double* aqq, size_t len, double* g);
 // result.rs:68-129 Gauss-Jordan; false when a pivot < 1e-15.
 bool invert_matrix(const Mat& m, Mat* out);
 

@@ -716,18 +716,9 @@ Mat Solver::jade(size_t max_iter, double tol) {
     for (size_t q = p + 1; q < n; ++q) pairs.emplace_back(p, q);
   auto chunk_lo = [&](size_t c) { return c * np / nch; };
   auto partial_g = [&](size_t p, size_t q, size_t c, double* g) {
-    const double* apq = A.data() + pos(p, q) * np;
-    const double* app = A.data() + pos(p, p) * np;
-    const double* aqq = A.data() + pos(q, q) * np;
-    double g00 = 0, g01 = 0, g11 = 0;
-    for (size_t m = chunk_lo(c); m < chunk_lo(c + 1); ++m) {
-      const double h_pq = apq[m] + apq[m];  // M(p,q) + M(q,p)
-      const double h_pp_qq = app[m] - aqq[m];
-      g00 += h_pq * h_pq;
-      g01 += h_pq * h_pp_qq;
-      g11 += h_pp_qq * h_pp_qq;
-    }
-    g[0] = g00; g[1] = g01; g[2] = g11;
+    const size_t m0 = chunk_lo(c);
+    jade_gsums(A.data() + pos(p, q) * np + m0, A.data() + pos(p, p) * np + m0, A.data() + pos(q, q) * np + m0,
+               chunk_lo(c + 1) - m0, g);
   };
   size_t sweeps_done = 0;
   bool converged = false;
@@ -787,11 +778,7 @@ Mat Solver::jade(size_t max_iter, double tol) {
             if (k == p || k == q) continue;
             double* ap = A.data() + (k < p ? pos(k, p) : pos(p, k)) * np;
             double* aq = A.data() + (k < q ? pos(k, q) : pos(q, k)) * np;
-            for (size_t m = m0; m < m1; ++m) {
-              const double mp = ap[m], mq = aq[m];
-              ap[m] = cs * mp - sn * mq;
-              aq[m] = sn * mp + cs * mq;
-            }
+            givens_rows(ap + m0, aq + m0, m1 - m0, cs, sn);
           }
           double* app = A.data() + pos(p, p) * np;
           double* apq = A.data() + pos(p, q) * np;
