@@ -1298,72 +1298,6 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
     }
 }
 
-// G_raw (, H_raw) tiles of 128×128 from the phase-1 fragments; blockIdx.x = tile, blockIdx.y = T split.
-template <bool NEED_H>
-__global__ void __launch_bounds__(FUSED_THREADS, 1)
-k_tiled_gram(const double* __restrict__ ybuf, const double* __restrict__ pbuf, const double* __restrict__ dbuf,
-             int ncp, uint64_t n_tiles, uint64_t tps, double* __restrict__ slabs, int accumulate) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int nib = ncp / 16;
-  const int nto = (nib + 7) / 8;  // output tiles per dimension
-  const int ti = blockIdx.x / nto, tj = blockIdx.x % nto;
-  const int gi0 = ti * 8 + (wave >> 2) * 4, gj0 = tj * 8 + (wave & 3) * 2;
-  d4 accg[4][2], acch[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) { accg[i][j] = d4{0, 0, 0, 0}; acch[i][j] = d4{0, 0, 0, 0}; }
-  bool iok[4], jok[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) iok[i] = gi0 + i < nib;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) jok[j] = gj0 + j < nib;
-  const uint64_t t_begin = (uint64_t)blockIdx.y * tps;
-  const uint64_t t_end = t_begin + tps < n_tiles ? t_begin + tps : n_tiles;
-  for (uint64_t tt = t_begin; tt < t_end; ++tt) {
-#pragma unroll 2
-    for (int t = 0; t < TL_TS; ++t) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double pa[4], da[4], yb[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const size_t f = tl_frag(tt, iok[i] ? gi0 + i : 0, t, r, nib) + lane;
-          pa[i] = iok[i] ? pbuf[f] : 0.0;
-          if constexpr (NEED_H) da[i] = iok[i] ? dbuf[f] : 0.0;
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const size_t f = tl_frag(tt, jok[j] ? gj0 + j : 0, t, r, nib) + lane;
-          yb[j] = jok[j] ? ybuf[f] : 0.0;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            accg[i][j] = mfma(pa[i], yb[j], accg[i][j]);
-            if constexpr (NEED_H) acch[i][j] = mfma(da[i], yb[j] * yb[j], acch[i][j]);
-          }
-      }
-    }
-  }
-  const size_t nsq = (size_t)ncp * ncp;
-  double* slab = slabs + (size_t)blockIdx.y * (NEED_H ? 2 : 1) * nsq;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      if (iok[i] && jok[j])
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = (gi0 + i) * 16 + lk + 4 * r, col = (gj0 + j) * 16 + lr;
-          const size_t o = (size_t)row * ncp + col;
-          slab[o] = accumulate ? slab[o] + accg[i][j][r] : accg[i][j][r];
-          if constexpr (NEED_H) slab[nsq + o] = accumulate ? slab[nsq + o] + acch[i][j][r] : acch[i][j][r];
-        }
-}
-
 // ---------------------------------------------------------------------------
 // Non-orthogonal line search in ONE pass (core.rs:117-140 with M = I + αD):
 // Y_α = (W + α·DW)·(X−μ) = Y + α·Z, so Y = W·(X−μ) and Z = (DW)·(X−μ) are
@@ -2294,7 +2228,7 @@ struct DeviceCtx : Evaluator {
                   int na, double* ll_out, double* y2_out) {
     HIP_OK(hipSetDevice(device));
     const int ncp = (int)((nc + 31) / 32 * 32);
-    const int ks = std::getenv("PICARD_MULTI_V1") ? 0 : yw_ks(nf);  // register-resident k_multi_loss2
+    const int ks = yw_ks(nf);  // nf ≤ 256: register-resident k_multi_loss2
     const int nfp = ks ? 4 * ks : (int)((nf + ML_KC - 1) / ML_KC * ML_KC);
     std::vector<double> wt((size_t)2 * nfp * ncp + ML_NA, 0.0);
     for (size_t i = 0; i < nc; ++i)
@@ -2439,12 +2373,7 @@ struct DeviceCtx : Evaluator {
     if (mode == 0) {
       const int nto = (ncp / 16 + 7) / 8;
       const uint64_t tps = (ntl + nsplit - 1) / nsplit;
-      if (std::getenv("PICARD_GRAM_V1")) {  // experiment knob: the unstaged phase 2
-        if (need_h)
-          k_tiled_gram<true><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
-        else
-          k_tiled_gram<false><<<dim3(nto * nto, nsplit), FUSED_THREADS, 0, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
-      } else {
+      {
         const size_t lds2 = (size_t)2 * (need_h ? 3 : 2) * 8 * 256 * sizeof(double);
         static bool attr2[2] = {false, false};
         auto k2 = need_h ? k_tiled_gram2<true> : k_tiled_gram2<false>;
@@ -2815,7 +2744,7 @@ struct DeviceCtx : Evaluator {
       dmu = ensure(d_mu, cap_mu, nf);
       HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
     }
-    const bool mfma_path = nc <= 64 && std::getenv("PICARD_MOMENTS_V1") == nullptr;
+    const bool mfma_path = nc <= 64;  // larger nc: the VALU tile kernel
     const uint64_t CH = mfma_path ? (1ull << 22) : (1ull << 16);
     // tiles of the upper triangle and the T split (≈ whole rounds of one workgroup per CU)
     const int nt = (np + 127) / 128;
