@@ -374,7 +374,8 @@ class TransformWorker {
 
 Solver::~Solver() = default;
 
-Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first) {  // core.rs:99-150
+Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first,
+                                     bool first_loss_only) {  // core.rs:99-150
   // Evaluation schedule: a try is a full fused pass, or a loss-only pass
   // completed (G, H, Σψ′) only if that try becomes the new iterate (both
   // bit-identical). Non-ortho searches evaluate their tries in one multi-α pass
@@ -450,7 +451,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       }
       no_multi_ = true;  // evaluator cannot: per-try passes from now on
     }
-    if (k == 0 && (first_full_ || !split_first_)) {
+    if (k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
     } else {
@@ -555,13 +556,19 @@ bool Solver::step() {
   }
   Mat direction = compute_direction(g, h, h_off, mem_, ortho);  // core.rs:334
   // non-ortho: all tries in one multi-α pass unless the last search accepted at try 1
-  LsResult res = line_search(direction, cfg_.ls_tries, !first_full_);
+  // Schedule only (never a decision): the first try's pass also yields the next
+  // gradient if it is accepted, so it is a full fused pass — unless the search
+  // direction is not a descent direction (⟨g, D⟩ ≥ 0: the loss rises for small
+  // α and the whole search almost surely fails), where a loss-only pass avoids
+  // the wasted G stage. An accepted try is completed either way.
+  const double slope = dot_sum(g, direction);
+  LsResult res = line_search(direction, cfg_.ls_tries, !first_full_, ortho && slope >= 0.0);
   const size_t first_tries = res.tries;
   const bool first_ok = res.success;
   first_full_ = res.success && res.tries == 1;
   if (!res.success) {  // core.rs:349-364
     mem_.clear();
-    res = line_search(scale(g, -1.0), 10, false);
+    res = line_search(scale(g, -1.0), 10, false, false);
   }
   if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
   if (res.needs_full) {  // rejected multi-try search kept as the iterate
@@ -570,9 +577,9 @@ bool Solver::step() {
     res.loss = loss_of(res.stats, res.w, signs_, &singular);
   }
   if (trace_) {
-    std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d\n",
+    std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
-                 res.partial ? 1 : 0);
+                 res.partial ? 1 : 0, slope);
   }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;

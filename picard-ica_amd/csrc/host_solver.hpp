@@ -47,7 +47,7 @@ class Solver {
   bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
   void complete(EvalStats* out);
   struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full; };
-  LsResult line_search(const Mat& direction, size_t tries, bool multi_first);
+  LsResult line_search(const Mat& direction, size_t tries, bool multi_first, bool first_loss_only);
   void init_core();
   Mat ica_par(const Mat& w_init);
   Mat jade(size_t max_iter, double tol);
