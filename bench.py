@@ -79,10 +79,26 @@ def cpu_baseline(n: int, t: int, seed: int, budget_s: float):
                       f"{last[0]} iterations in {last[1]:.2f}s; OpenBLAS dgemm threads={cores}, elementwise 1 thread"}
 
 
+def relaunch_distributed(gpus: int) -> int:
+    """`python bench.py --gpus N` without a launcher: run the same command under
+    torch.distributed.run (one rank per GPU) as a child process — before anything
+    here touches a GPU — and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n, T = args.n, int(args.t)
 
