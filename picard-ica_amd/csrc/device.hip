@@ -204,8 +204,10 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 //   tanh  Σψ′ = α·(n − Σ th²)               (ψ′ = α(1 − th²))
 //         Σℓ  = Σ|y| + (n·ln2 + ln Π(1 + em/2))/α   (ℓ = |y| + ln(2 + em)/α)
 //         the product replaces one fp64 log per element by one multiply; it is
-//         kept as mantissa × 2^e (renormalised once per block) and its log is
-//         taken once per lane
+//         accumulated as Π(2 + em) (the divisor of tanh's rcp, so no extra op),
+//         kept as mantissa × 2^e (renormalised every 32 blocks: factors ∈ (1, 2])
+//         and its log is taken once per lane, minus (#factors)·ln2 — the same
+//         bits as Π(1 + em/2), since halving is exact
 //   exp   Σψ′ = n + Σ(em − α y² k),  Σℓ = −(n + Σ em)/α   (k = e^{−αy²/2} = 1 + em)
 //   cube  Σψ′ = 3·Σy²,  Σℓ = Σ y⁴/4
 // All kernels of this family share these formulas and the sample → lane map,
@@ -213,18 +215,44 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
 // ---------------------------------------------------------------------------
 struct RowAcc {
   double d = 0.0, l = 0.0, q = 0.0;  // raw Σψ′ term, raw Σℓ term, Σy²
-  double p = 1.0;                    // tanh: Π (1 + em/2), mantissa
-  int e = 0;                         //       … and binary exponent
+  double p = 1.0;                    // tanh: Π (2 + em), mantissa
+  int e = 0;                         //       … and its binary exponent
 };
 
-// e^x for NW independent x ∈ [−708, 0] as sc·(1 + emr), sc = 2^k, |r| ≤ ln2/2,
-// written step-interleaved so the NW dependent FMA chains overlap (left to
-// itself the compiler emits them one after another). Rounding to k uses the
-// 1.5·2^52 shifter (its low word IS k, so 2^k is built with one integer op);
-// the reduction r = x − k·ln2 is a single fma: its error |k|·2^-56·e^x stays
-// ≤ 1.2e-17 absolute for x ≤ 0, and is 0 for k = 0 (small |y|).
+// e^x table for exp_n: T_j = 2^(j/32) (correctly rounded), with the high word
+// pre-biased by −(j << 15) so that adding (m << 15) for m = 32k + j yields
+// the high word of 2^k·T_j in ONE integer op (mod 2^32). Every kernel that
+// calls exp_n copies it into its own LDS (exp_tab_load, before the first
+// barrier): 32 doubles = the 64 LDS banks once, so any lane pattern is
+// conflict-free.
+__constant__ uint64_t c_exp_tab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+#define EXP_TAB_DECL __shared__ double s_exp_tab[32]
+constexpr int EXP_TAB_BYTES = 32 * sizeof(double);  // static LDS: the dynamic limit is 160 KiB minus this
+__device__ __forceinline__ void exp_tab_load(double* tab) {
+  if (threadIdx.x < 32) tab[threadIdx.x] = __longlong_as_double((long long)c_exp_tab[threadIdx.x]);
+}
+
+// e^x for NW independent x ∈ [−708, 0] as s·(1 + emr), s = 2^(m/32) from the
+// LDS table, |r| ≤ ln2/64, written step-interleaved so the NW dependent FMA
+// chains overlap (left to itself the compiler emits them one after another).
+// Rounding to m uses the 1.5·2^52 shifter (its low word IS m); the reduction
+// r = x − m·ln2/32 is one fma (error ≤ |m|·2^-59·e^x ≤ 3e-17 absolute for
+// x ≤ 0, 0 for m = 0); e^r − 1 = r + r²·p(r), p of degree 4 (near-minimax on
+// |r| ≤ ln2/64, mpmath chebyfit: ≤ 2.2e-19 absolute). 15 VALU + 1 LDS read per
+// element against 19 for the table-free degree-11 form.
+// Table-free variant (sc = 2^k, |r| ≤ ln2/2, degree-11 e^r − 1): 19 VALU per
+// element, no LDS read and fewer live registers — for kernels at the edge of
+// their VGPR budget (k_multi_loss2 at nf = 256).
 template <int NW>
-__device__ __forceinline__ void exp_n(const double* x, double* emr, double* sc) {
+__device__ __forceinline__ void exp_n_poly(const double* x, double* emr, double* sc) {
   constexpr double SHIFT = 0x1.8p52;
   double t[NW], r[NW], p[NW];
 #pragma unroll
@@ -249,14 +277,41 @@ __device__ __forceinline__ void exp_n(const double* x, double* emr, double* sc) 
   }
 }
 
+template <int NW>
+__device__ __forceinline__ void exp_n(const double* x, const double* tab, double* emr, double* sc) {
+  constexpr double SHIFT = 0x1.8p52;
+  constexpr double LOG2E_32 = 0x1.71547652b82fep+5, LN2_32 = 0x1.62e42fefa39efp-6;
+  double t[NW], r[NW], p[NW], tj[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t[i] = __builtin_fma(x[i], LOG2E_32, SHIFT);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) tj[i] = tab[__double2loint(t[i]) & 31];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r[i] = __builtin_fma(-(t[i] - SHIFT), LN2_32, x[i]);
+  constexpr double C[5] = {0x1.6c16ffe57d9c9p-10, 0x1.11114f8a7941cp-7, 0x1.555555555194dp-5,
+                           0x1.555555554dd45p-3, 0x1.0000000000000p-1};
+#pragma unroll
+  for (int i = 0; i < NW; ++i) p[i] = __builtin_fma(C[0], r[i], C[1]);
+#pragma unroll
+  for (int c = 2; c < 5; ++c)
+#pragma unroll
+    for (int i = 0; i < NW; ++i) p[i] = __builtin_fma(p[i], r[i], C[c]);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    emr[i] = __builtin_fma(r[i] * r[i], p[i], r[i]);
+    const int m = __double2loint(t[i]);
+    sc[i] = __hiloint2double(__double2hiint(tj[i]) + (m << 15), __double2loint(tj[i]));
+  }
+}
+
 // ψ (and ψ′ if NEED_D) of one 4-element fragment, NW elements interleaved at a
 // time (register budget); accumulates the row terms in element order, so the
 // sums do not depend on NW. Σy² only if NEED_Q (the reference uses Y∘Y only in
 // non-orthogonal mode; cube needs it for Σψ′). m2a = −2α.
 // th = −em/(2+em) uses one Newton step on v_rcp_f64 (≲ 10 ulp).
 template <int DENS, bool NEED_D, bool NEED_Q, int NW = 4>
-__device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m2a, RowAcc& a, double (&psi)[4],
-                                             double (&dpsi)[4]) {
+__device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m2a, const double* tab, RowAcc& a,
+                                             double (&psi)[4], double (&dpsi)[4]) {
   if constexpr (NEED_Q || DENS == DENS_CUBE)
 #pragma unroll
     for (int i = 0; i < 4; ++i) a.q = __builtin_fma(y[i], y[i], a.q);
@@ -266,22 +321,23 @@ __device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) x[i] = fmax(m2a * fabs(y[g + i]), -708.0);  // = −2|αy| exactly (α > 0)
-      exp_n<NW>(x, emr, sc);
+      exp_n<NW>(x, tab, emr, sc);
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
         const double em = __builtin_fma(sc[i], emr[i], sc[i] - 1.0);  // e^{-2α|y|} − 1 ∈ (−1, 0]
-        const double th = copysign(-em * fm::rcp_nr1(2.0 + em), y[g + i]);
+        const double q = 2.0 + em;                                     // ∈ (1, 2], exactly 2 at y = 0
+        const double th = copysign(-em * fm::rcp_nr1(q), y[g + i]);
         psi[g + i] = th;
         a.d = __builtin_fma(th, th, a.d);
         if constexpr (NEED_D) dpsi[g + i] = alpha * __builtin_fma(-th, th, 1.0);
         a.l += fabs(y[g + i]);
-        a.p *= __builtin_fma(em, 0.5, 1.0);  // ∈ (0.5, 1], exactly 1 at y = 0
+        a.p *= q;
       }
     } else if constexpr (DENS == DENS_EXP) {
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) x[i] = fmax(-alpha / 2.0 * (y[g + i] * y[g + i]), -708.0);
-      exp_n<NW>(x, emr, sc);
+      exp_n<NW>(x, tab, emr, sc);
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
         const double y2 = y[g + i] * y[g + i];
@@ -312,8 +368,8 @@ __device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m
 }
 
 // ℓ terms only (line-search tries): identical arithmetic to density_acc4's ℓ part
-template <int DENS, bool NEED_Q, int NW = 4>
-__device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a, RowAcc& a) {
+template <int DENS, bool NEED_Q, int NW = 4, bool TAB = true>
+__device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a, const double* tab, RowAcc& a) {
   if constexpr (NEED_Q || DENS == DENS_CUBE)  // as density_acc4 (cube's fused pass keeps Σy²)
 #pragma unroll
     for (int i = 0; i < 4; ++i) a.q = __builtin_fma(y[i], y[i], a.q);
@@ -323,18 +379,19 @@ __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a,
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) x[i] = fmax(m2a * fabs(y[g + i]), -708.0);
-      exp_n<NW>(x, emr, sc);
+      if constexpr (TAB) exp_n<NW>(x, tab, emr, sc); else exp_n_poly<NW>(x, emr, sc);
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
         const double em = __builtin_fma(sc[i], emr[i], sc[i] - 1.0);
         a.l += fabs(y[g + i]);
-        a.p *= __builtin_fma(em, 0.5, 1.0);
+        a.p *= 2.0 + em;
       }
+      if constexpr (TAB) __builtin_amdgcn_sched_barrier(0);  // one group's chain live at a time
     } else if constexpr (DENS == DENS_EXP) {
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) x[i] = fmax(-alpha / 2.0 * (y[g + i] * y[g + i]), -708.0);
-      exp_n<NW>(x, emr, sc);
+      if constexpr (TAB) exp_n<NW>(x, tab, emr, sc); else exp_n_poly<NW>(x, emr, sc);
 #pragma unroll
       for (int i = 0; i < NW; ++i) a.l += __builtin_fma(sc[i], emr[i], sc[i]) - 1.0;
     } else if constexpr (DENS == DENS_CUBE) {
@@ -347,7 +404,9 @@ __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a,
   }
 }
 
-// every few blocks (≤ 64 factors ≥ 1/2 since the last call: no underflow)
+// every ≤ 32 blocks (≤ 128 factors ∈ (1, 2] since the last call: no overflow);
+// frexp is exact, so the cadence does not change any bits
+constexpr int RENORM_BLOCKS = 32;
 template <int DENS>
 __device__ __forceinline__ void acc_renorm(RowAcc& a) {
   if constexpr (DENS == DENS_TANH) {
@@ -358,10 +417,14 @@ __device__ __forceinline__ void acc_renorm(RowAcc& a) {
 }
 
 // per-lane raw Σℓ term (before the cross-lane sums)
+// (nfac = number of factors in the tanh product: 4 per density call)
 template <int DENS>
-__device__ __forceinline__ double acc_ll(const RowAcc& a, double inv_alpha) {
-  if constexpr (DENS == DENS_TANH)
-    return __builtin_fma(__builtin_fma((double)a.e, fm::LN2, log(a.p)), inv_alpha, a.l);
+__device__ __forceinline__ double acc_ll(const RowAcc& a, double inv_alpha, int nfac) {
+  if constexpr (DENS == DENS_TANH) {
+    int ex;  // final renormalisation: (mantissa, exponent) no longer depends on the cadence
+    const double m = frexp(a.p, &ex);
+    return __builtin_fma(__builtin_fma((double)(a.e + ex - nfac), fm::LN2, log(m)), inv_alpha, a.l);
+  }
   else
     return a.l;
 }
@@ -445,6 +508,8 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
 
   extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
   double* xs0 = smem;             // [2][TS][NFP][16]
   double* img0 = smem + 2 * XS;   // [2][NIMG][KK][NB][64]
 
@@ -524,7 +589,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   // density on the tile, row terms, hand-off of the ψ / y (/ ψ′) fragments
   auto elementwise = [&](const d4& yv, double* img) {
     double psi[4], dpsi[4];
-    density_acc4<DENS, NEED_H, NEED_Q, FUSED_NW>(yv, alpha, m2a, racc, psi, dpsi);
+    density_acc4<DENS, NEED_H, NEED_Q, FUSED_NW>(yv, alpha, m2a, s_exp_tab, racc, psi, dpsi);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
@@ -577,14 +642,17 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
       const d4 yv = y_stage(xs0 + (cur ^ 1) * XS);     // block b+1
       g_stage(img0 + cur * NIMG * S::FRAGS);           // block b
       elementwise(yv, img0 + (cur ^ 1) * NIMG * S::FRAGS);
-      if (cur) acc_renorm<DENS>(racc);  // every second block
       store_x(clampb(b + 2), xs0 + cur * XS, use);
       __syncthreads();
     };
     uint64_t b = b_begin;
-    for (; b + 1 < b_last; b += 2) {
-      iter(b, 0, preA, preB);
-      iter(b + 1, 1, preB, preA);
+    while (b + 1 < b_last) {  // chunks of RENORM_BLOCKS blocks, renormalised after each
+      const uint64_t lim = b + RENORM_BLOCKS < b_last ? b + RENORM_BLOCKS : b_last;
+      for (; b + 1 < lim; b += 2) {
+        iter(b, 0, preA, preB);
+        iter(b + 1, 1, preB, preA);
+      }
+      acc_renorm<DENS>(racc);
     }
     int cur = 0;
     if (b < b_last) {
@@ -636,7 +704,8 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     __syncthreads();
   }
   // row sums: over the 4 lane groups, then over the TS waves of one row block
-  double rs_dpsi = acc_dpsi<DENS>(racc), rs_ll = acc_ll<DENS>(racc, inv_alpha), rs_y2 = racc.q;
+  const int nfac = b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0;  // one density call per block
+  double rs_dpsi = acc_dpsi<DENS>(racc), rs_ll = acc_ll<DENS>(racc, inv_alpha, nfac), rs_y2 = racc.q;
   rs_dpsi += __shfl_xor(rs_dpsi, 16); rs_dpsi += __shfl_xor(rs_dpsi, 32);
   rs_ll += __shfl_xor(rs_ll, 16);     rs_ll += __shfl_xor(rs_ll, 32);
   rs_y2 += __shfl_xor(rs_y2, 16);     rs_y2 += __shfl_xor(rs_y2, 32);
@@ -655,6 +724,22 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     orow[c * NCP + row] = sum;
   }
 }
+
+// ---------------------------------------------------------------------------
+// Warp-specialised fused pass for NB = 8 (64 < nc ≤ 128, no H), 16 waves:
+//   waves 0-7  ("Y waves"): Y stage + density of row block w (W fragment in
+//              VGPRs), ψ / y fragments → LDS images;
+//   waves 8-15 ("G waves"): the G tiles of k_eval_fused<8> (GI = 4 × GJ = 2
+//              accumulators in VGPRs) and the X staging (global → registers →
+//              X − μ → LDS, prefetched a full iteration ahead).
+// k_eval_fused<8> holds both roles in every wave (256 VGPRs: 2 waves per SIMD,
+// the barrier and MFMA → VALU latencies exposed); split, each role fits 128
+// VGPRs and a CU runs 4 waves per SIMD. Each role runs its own loop (so the W
+// fragments and the accumulators are never live at once) with the same number
+// of barriers. Same block partition, G-tile map, k order, lane map and row-term
+// formulas as k_eval_fused<8> / k_eval_loss<8> / k_eval_fromy<8>: identical sums.
+// ---------------------------------------------------------------------------
+#include "fused_ws.inc"
 
 // ---------------------------------------------------------------------------
 // Split evaluation for line-search tries (bit-identical sums to k_eval_fused):
@@ -678,14 +763,21 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
   const int yi = wave % NB, yts = wave / NB;
   const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
   extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
   double* xs0 = smem;  // [2][TS][NFP][16]
   double wf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) wf[ks] = Wp[(yi * 16 + lr) * NFP + 4 * ks + lk];
   RowAcc racc;
+  // this workgroup's blocks b_begin + i, i < nb; block indices are 32-bit and
+  // wave-uniform inside the loop (scalar compares, no 64-bit VALU compares
+  // holding VGPRs); blocks i < nfull hold no padding
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
-  const uint64_t b_last = b_end - 1;
+  const uint32_t nb = b_begin < b_end ? (uint32_t)(b_end - b_begin) : 0u;
+  const uint64_t nfull_g = n_local / TB;
+  const uint32_t nfull = nfull_g > b_begin ? (uint32_t)(nfull_g - b_begin < nb ? nfull_g - b_begin : nb) : 0u;
   int xk[PRE], xt[PRE];
   double xmu[PRE];
   const double* xsrc[PRE];
@@ -696,18 +788,18 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
     xt[p] = 2 * (e % (TB / 2));
     const bool ok = xk[p] < nf;
     xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
-    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
+    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p] + b_begin * TB;
   }
   // one prefetch register set (128-VGPR budget): X(b+1) is requested at the top
   // of iteration b — pinned there by a scheduling barrier — and consumed after
   // the Y stage and the density math of block b, which hide its HBM latency
   double2 pre[PRE];
-  auto load_x = [&](uint64_t b) {
+  auto load_x = [&](uint32_t i) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * TB);
+    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + (size_t)i * TB);
   };
-  auto store_x = [&](uint64_t b, double* xs) {
-    if (b * TB + TB <= n_local) {
+  auto store_x = [&](uint32_t i, double* xs) {
+    if (i < nfull) {
 #pragma unroll
       for (int p = 0; p < PRE; ++p) {
         const double2 v = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
@@ -716,7 +808,7 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
     } else {
 #pragma unroll
       for (int p = 0; p < PRE; ++p) {
-        const uint64_t tg = b * TB + xt[p];
+        const uint64_t tg = (b_begin + i) * TB + xt[p];
         double2 v;
         v.x = tg < n_local ? pre[p].x - xmu[p] : 0.0;
         v.y = tg + 1 < n_local ? pre[p].y - xmu[p] : 0.0;
@@ -724,31 +816,38 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
       }
     }
   };
-  auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
-  if (b_begin < b_end) {
-    load_x(b_begin);
-    store_x(b_begin, xs0);
+  if (nb > 0) {
+    load_x(0);
+    store_x(0, xs0);
     __syncthreads();
     int cur = 0;
-    for (uint64_t b = b_begin; b < b_end; ++b) {
-      load_x(clampb(b + 1));
-      __builtin_amdgcn_sched_barrier(0);
-      d4 yv = d4{0, 0, 0, 0};  // one chain, same order as k_eval_fused's Y stage
-      const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
+    // chunks of RENORM_BLOCKS blocks, the product renormalised after each (a
+    // loop-level call, so it costs no per-block selects)
+    for (uint32_t c0 = 0; c0 < nb; c0 += RENORM_BLOCKS) {
+      const uint32_t c1 = c0 + RENORM_BLOCKS < nb ? c0 + RENORM_BLOCKS : nb;
+      for (uint32_t i = c0; i < c1; ++i) {
+        const uint32_t inext = i + 1 < nb ? i + 1 : nb - 1;  // clamped: always a valid address
+        load_x(inext);
+        __builtin_amdgcn_sched_barrier(0);
+        d4 yv = d4{0, 0, 0, 0};  // one chain, same order as k_eval_fused's Y stage
+        const double* xrow = xs0 + cur * XS + (yts * NFP + lk) * 16 + lr;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
-      loss_acc4<DENS, NEED_Q, LOSS_NW>(yv, alpha, m2a, racc);
-      if constexpr (STORE)
+        for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
+        // X(i+1) → the other buffer before the density math (its load had the
+        // whole MFMA chain to land), so nothing of the density is sunk past the
+        // staging branch and no table value stays live across it
+        store_x(inext, xs0 + (cur ^ 1) * XS);
+        loss_acc4<DENS, NEED_Q, LOSS_NW>(yv, alpha, m2a, s_exp_tab, racc);
+        if constexpr (STORE)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ybuf[((b * 8 + wave) * 4 + r) * 64 + lane] = yv[r];
-      if (cur) acc_renorm<DENS>(racc);  // every second block
-      __builtin_amdgcn_sched_barrier(0);  // consume X(b+1) only after the density math
-      store_x(clampb(b + 1), xs0 + (cur ^ 1) * XS);
-      __syncthreads();
-      cur ^= 1;
+          for (int r = 0; r < 4; ++r) ybuf[(((b_begin + i) * 8 + wave) * 4 + r) * 64 + lane] = yv[r];
+        __syncthreads();
+        cur ^= 1;
+      }
+      acc_renorm<DENS>(racc);
     }
   }
-  double rs_ll = acc_ll<DENS>(racc, inv_alpha), rs_y2 = racc.q;
+  double rs_ll = acc_ll<DENS>(racc, inv_alpha, 4 * (int)nb), rs_y2 = racc.q;
   rs_ll += __shfl_xor(rs_ll, 16); rs_ll += __shfl_xor(rs_ll, 32);
   rs_y2 += __shfl_xor(rs_y2, 16); rs_y2 += __shfl_xor(rs_y2, 32);
   double* rsb = xs0;  // [TS][NCP][2]
@@ -778,6 +877,9 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
   const int yi = wave % NB, yts = wave / NB;
   const double inv_alpha = 1.0 / alpha;
   extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
+  __syncthreads();  // the first density call precedes the pipeline's first barrier
   double* img0 = smem;  // [2][NIMG][KK][NB][64]
   int gi0, gj0, kk0;
   if constexpr (NB == 8) { gi0 = (wave >> 2) * 4; gj0 = (wave & 3) * 2; kk0 = 0; }
@@ -803,7 +905,7 @@ k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, ui
   };
   auto elementwise = [&](const d4& yv, double* img) {
     double psi[4], dpsi[4];
-    density_acc4<DENS, NEED_H, false, FROMY_NW>(yv, alpha, -2.0 * alpha, racc, psi, dpsi);  // ℓ, Σy² terms unused
+    density_acc4<DENS, NEED_H, false, FROMY_NW>(yv, alpha, -2.0 * alpha, s_exp_tab, racc, psi, dpsi);  // ℓ, Σy² terms unused
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = ((yts * 4 + r) * NB + yi) * 64 + lane;
@@ -1097,6 +1199,8 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   const int row = ib * 16 + lr;
   const double alpha_ = alpha, inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
   extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
   double* xs0 = smem;  // [2][NFP][16]
   double wf[KS];
 #pragma unroll
@@ -1156,7 +1260,7 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
         for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
         if constexpr (MODE == 0) {
           double psi[4], dpsi[4];
-          density_acc4<DENS, true, true, 1>(yv, alpha_, m2a, racc, psi, dpsi);
+          density_acc4<DENS, true, true, 1>(yv, alpha_, m2a, s_exp_tab, racc, psi, dpsi);
           const uint64_t tt = b >> 2;
           const int ts = (int)(b & 3);
 #pragma unroll
@@ -1167,9 +1271,9 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
             if (dbuf) dbuf[f] = dpsi[r];
           }
         } else {
-          loss_acc4<DENS, true, 1>(yv, alpha_, m2a, racc);
+          loss_acc4<DENS, true, 1>(yv, alpha_, m2a, s_exp_tab, racc);
         }
-        if (b & 1) acc_renorm<DENS>(racc);
+        if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc);
       }
       __builtin_amdgcn_sched_barrier(0);
       store_x(b < b_last ? b + 1 : b_last, xs0 + (cur ^ 1) * XS);
@@ -1179,7 +1283,8 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   }
   // raw row terms → workgroup partials [Σψ′ | Σℓ | Σy²] (ncp each); the two
   // roles of a slot write disjoint rows
-  double rs_d = acc_dpsi<DENS>(racc), rs_l = acc_ll<DENS>(racc, inv_alpha), rs_q = racc.q;
+  const int nfac = b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0;  // one density call per block
+  double rs_d = acc_dpsi<DENS>(racc), rs_l = acc_ll<DENS>(racc, inv_alpha, nfac), rs_q = racc.q;
   rs_d += __shfl_xor(rs_d, 16); rs_d += __shfl_xor(rs_d, 32);
   rs_l += __shfl_xor(rs_l, 16); rs_l += __shfl_xor(rs_l, 32);
   rs_q += __shfl_xor(rs_q, 16); rs_q += __shfl_xor(rs_q, 32);
@@ -1451,6 +1556,8 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
   const int row = ib * 16 + lr;
   const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
   extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
   double* xs0 = smem;             // [2][NFP][16]
   double* ex0 = smem + 2 * XS;    // [2][2 K-halves][4 row blocks][Y, Z][4][64]
   double wf[KH], zf[KH];
@@ -1544,8 +1651,8 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
             d4 yj;
 #pragma unroll
             for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj[u], zv[r], yv[r]);
-            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, racc[u]);
-            if (b & 1) acc_renorm<DENS>(racc[u]);
+            loss_acc4<DENS, NEED_Q, 1, (KS < 64)>(yj, alpha, m2a, s_exp_tab, racc[u]);  // KS = 64: no table (VGPRs)
+            if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
           }
         }
       }
@@ -1557,7 +1664,7 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
 #pragma unroll
   for (int u = 0; u < ML2_TRIES; ++u) {
     if (u < my_na) {
-      double l = acc_ll<DENS>(racc[u], inv_alpha), q = racc[u].q;
+      double l = acc_ll<DENS>(racc[u], inv_alpha, b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0), q = racc[u].q;
       l += __shfl_xor(l, 16); l += __shfl_xor(l, 32);
       q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
       if (active && lk == 0) {
@@ -2111,14 +2218,22 @@ struct DeviceCtx : Evaluator {
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
     (void)nfp;
-    auto kern = k_eval_fused<NB, H, D, Q>;
+    // NB = 8 without H: the warp-specialised 16-wave kernel (same sums);
+    // PICARD_FUSED_WS=0 selects the 8-wave k_eval_fused<8> (A/B timing)
+    static const bool ws_on = [] {
+      const char* e = std::getenv("PICARD_FUSED_WS");
+      return !(e && e[0] == '0');
+    }();
+    const bool ws = NB == 8 && !H && ws_on;
+    auto kern = ws ? k_eval_fused_ws<D, Q> : k_eval_fused<NB, H, D, Q>;
     static bool attr_set = false;
     if (!attr_set) {
-      HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
       attr_set = true;
     }
     HIP_OK(hipEventRecord(ev[1], stream));
-    kern<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part);
+    kern<<<nwg, ws ? WS_THREADS : FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw,
+                                                                n_blocks, part);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t total = EvalStats::size(nc, H);
@@ -2208,7 +2323,7 @@ struct DeviceCtx : Evaluator {
     auto k = want_y2 ? k_multi_loss2<KS, D, true> : k_multi_loss2<KS, D, false>;
     static bool attr[2] = {false, false};
     if (!attr[want_y2]) {
-      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
       attr[want_y2] = true;
     }
     k<<<dim3(nwg, nroles), FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, ncp, dw, dz, dmu, alpha, dal, na,
@@ -2332,7 +2447,7 @@ struct DeviceCtx : Evaluator {
     auto k = mode == 0 ? k_tiled_yw<KS, D, 0> : k_tiled_yw<KS, D, 1>;
     static bool attr[2] = {false, false};
     if (!attr[mode]) {
-      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
       attr[mode] = true;
     }
     k<<<dim3(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, n_in, (int)nf, ncp, d_w, dmu, alpha, bpw,

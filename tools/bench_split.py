@@ -11,7 +11,8 @@ dens = sys.argv[4] if len(sys.argv) > 4 else "tanh"
 ctx = pa.DeviceContext(0)
 ctx.generate(n, t, 42)
 mu = ctx.rowsum() / t
-w = np.linalg.qr(np.random.default_rng(0).normal(size=(n, n)))[0] * 0.05
+scale = float(sys.argv[5]) if len(sys.argv) > 5 else 0.05
+w = np.linalg.qr(np.random.default_rng(0).normal(size=(n, n)))[0] * scale
 d = {"tanh": pa.DensityType.tanh(), "exp": pa.DensityType.exp(), "cube": pa.DensityType.cube()}[dens]
 ctx.eval(w, mu, d, False, need_y2=False); ctx.eval_split(w, mu, d, False, need_y2=False)
 ctx.kernel_breakdown(reset=True)

@@ -1,0 +1,37 @@
+"""Per-kernel effective clock and issue mix from a rocprofv3 --kernel-trace --pmc run.
+Usage: python tools/clock_summary.py DIR   (DIR holds run_counter_collection.csv, run_kernel_trace.csv)
+clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md 'DVFS give-back')."""
+import collections
+import csv
+import os
+import sys
+
+d = sys.argv[1]
+dur = {}
+for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
+    dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+per = collections.defaultdict(dict)
+names = {}
+for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+    k = r["Dispatch_Id"]
+    names[k] = r["Kernel_Name"].split("(")[0]
+    per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for k, c in per.items():
+    if "k_eval" not in names[k] and "k_multi" not in names[k] and "k_tiled" not in names[k]:
+        continue
+    ns = dur.get(k)
+    if not ns or ns < 1e6:
+        continue
+    a = agg[names[k]]
+    a["ms"].append(ns / 1e6)
+    a["clock_ghz"].append(c["GRBM_GUI_ACTIVE"] / 8 / ns)
+    for key in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES",
+                "SQ_ACTIVE_INST_VALU", "SQ_INSTS_LDS", "SQ_WAIT_INST_ANY"):
+        a[key].append(c.get(key, float("nan")))
+for name, a in agg.items():
+    m = {k: sum(v) / len(v) for k, v in a.items()}
+    print(f"{name}: launches={len(a['ms'])} ms={m['ms']:.2f} clock={m['clock_ghz']:.3f} GHz "
+          f"valu/mfma={m['SQ_INSTS_VALU'] / max(m['SQ_INSTS_MFMA'], 1):.2f} "
+          f"mfma_busy/busy={m['SQ_VALU_MFMA_BUSY_CYCLES'] / max(m['SQ_BUSY_CYCLES'], 1):.3f} "
+          + " ".join(f"{k}={m[k]:.4g}" for k in sorted(m) if k.startswith("SQ_")))
