@@ -188,7 +188,7 @@ def main():
                 pmc = p.get("kernels", {})
         except Exception:
             pass
-    kinds = {"fused": ("k_eval_fused", "k_eval_fused<8,false,tanh,noY2>", 4.0),
+    kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2>", 4.0),
              "loss": ("k_eval_loss", "k_eval_loss<8,tanh,nostore,noY2>", 2.0)}
     rooflines = []
     for kind, (short, label, c) in kinds.items():

@@ -22,8 +22,11 @@ def main():
             for row in csv.DictReader(f):
                 name = row["Kernel_Name"]
                 for short in KERNELS:
-                    # the solver's instantiations: tanh, no H (and no Σy²)
-                    if short in name and name.split("<")[1].startswith("8, "):
+                    # the solver's instantiations: tanh, no H (and no Σy²); the fused pass at
+                    # 64 < nc <= 128 is the warp-specialised k_eval_fused_ws<dens, Q>
+                    tmpl = name.split("<")[1] if "<" in name else ""
+                    if short in name and (tmpl.startswith("8, ") or
+                                          (short == "k_eval_fused" and "k_eval_fused_ws<0," in name)):
                         vals[(short, name.split("(")[0])][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {"n": n, "t_local": t_local, "sources": sys.argv[4:], "kernels": {}}
     for short in KERNELS:
