@@ -1873,6 +1873,24 @@ __global__ void __launch_bounds__(256) k_rowsum(const double* __restrict__ X, ui
   (void)n_local;  // columns past n_local are zero (alloc_x zero-fills the padding)
 }
 
+// Resident-X centring: X[k][t] ← X[k][t] − μ[k] (UNDO: + μ[k]) for t < n_local,
+// the padding left at zero. The subtraction is the one every pass kernel would
+// otherwise do while staging X, so the centred X is bit-identical to it.
+template <bool UNDO>
+__global__ void __launch_bounds__(256) k_shift_rows(double* __restrict__ X, uint64_t ldx, uint64_t n_local,
+                                                    const double* __restrict__ mu) {
+  const int k = blockIdx.y;
+  const double m = mu[k];
+  double* row = X + (size_t)k * ldx;
+  for (uint64_t t = 2 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); t < n_local;
+       t += 2 * (uint64_t)gridDim.x * blockDim.x) {
+    double2 v = *reinterpret_cast<double2*>(row + t);
+    v.x = UNDO ? v.x + m : v.x - m;
+    if (t + 1 < n_local) v.y = UNDO ? v.y + m : v.y - m;
+    *reinterpret_cast<double2*>(row + t) = v;
+  }
+}
+
 // Fourth moments for JADE: out[p][q] += Σ_t z_p z_q, z_(i≤j) = y_i y_j, over a Y chunk.
 __global__ void __launch_bounds__(256) k_moments4(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc,
                                                   const int* __restrict__ pi, const int* __restrict__ pj, int np,
@@ -2076,7 +2094,7 @@ struct DeviceCtx : Evaluator {
   ~DeviceCtx() override {
     (void)hipSetDevice(device);
     if (comm) ncclCommDestroy(comm);
-    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow})
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part})
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -2099,6 +2117,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     if (X) HIP_OK(hipFree(X));
     nf = nf_; n_local_ = n_local; n_total = n_tot; t0 = t0_;
+    xshift_.clear();
+    raw_sums_.clear();
     ldx = (n_local + 127) / 128 * 128;  // a fused-pass tile (≤ 128 samples) never crosses a row end
     if (ldx == 0) ldx = 128;
     HIP_OK(hipMalloc(&X, nf * ldx * sizeof(double) + 256));
@@ -2115,6 +2135,7 @@ struct DeviceCtx : Evaluator {
 
   void download(double* out) {
     HIP_OK(hipSetDevice(device));
+    unshift_x();  // the caller's data (up to rounding if it was centred in place)
     if (n_local_)
       HIP_OK(hipMemcpy2DAsync(out, n_local_ * sizeof(double), X, ldx * sizeof(double), n_local_ * sizeof(double),
                               nf, hipMemcpyDeviceToHost, stream));
@@ -2163,21 +2184,73 @@ struct DeviceCtx : Evaluator {
     if (world > 1) RCCL_OK(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm, stream));
   }
 
-  void rowsum(double* out) override {
-    HIP_OK(hipSetDevice(device));
+  // this shard's row sums of the resident X into st (device), no all-reduce;
+  // partials in *part_buf (grown as needed)
+  void local_rowsum(double* st, double*& part_buf, size_t& part_cap) {
     // ≥ 8 workgroups per CU in total, slices a multiple of 512 samples (16-B loads)
     const uint64_t slices = std::max<uint64_t>(1, std::min<uint64_t>((ldx + 511) / 512,
                                                                      (uint64_t)(8 * n_cu + nf - 1) / nf));
     const uint64_t per = ((ldx + slices - 1) / slices + 511) / 512 * 512;
     const int nwg = (int)((ldx + per - 1) / per);
-    double* part = ensure(d_part, cap_part, (size_t)nwg * nf);
-    double* st = ensure(d_stats, cap_stats, nf);
+    double* part = ensure(part_buf, part_cap, (size_t)nwg * nf);
     k_rowsum<<<dim3(nwg, (unsigned)nf), 256, 0, stream>>>(X, ldx, n_local_, (int)nf, per, part);
     HIP_OK(hipGetLastError());
     k_sum_slabs<<<(nf + 255) / 256, 256, 0, stream>>>(part, nwg, nf, st);
+    HIP_OK(hipGetLastError());
+  }
+
+  void rowsum(double* out) override {
+    HIP_OK(hipSetDevice(device));
+    double* st = ensure(d_stats, cap_stats, nf);
+    if (xshift_.empty()) local_rowsum(st, d_part, cap_part);
+    else  // centred in place: the sums of the caller's data, kept from before the shift
+      HIP_OK(hipMemcpyAsync(st, raw_sums_.data(), nf * sizeof(double), hipMemcpyHostToDevice, stream));
     allreduce(st, nf);
     HIP_OK(hipMemcpyAsync(out, st, nf * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  // Resident-X centring. Every pass computes Y = W·(X − μ); instead of
+  // subtracting μ while staging X in every pass, the first call with a given μ
+  // subtracts it from the resident X in place (k_shift_rows: the same fp64
+  // subtraction, so the passes read bit-identical X − μ) and the kernels then
+  // run with μ = null. A call with another μ (or none) first restores X by
+  // adding the old μ back, which is exact only up to rounding — the solver
+  // always passes one μ per fit, so its passes never hit that path.
+  std::vector<double> xshift_;  // μ currently subtracted from the resident X (empty: none)
+  std::vector<double> raw_sums_;  // this shard's row sums of X before the shift
+  double* d_shift_sum = nullptr; size_t cap_shift_sum = 0;
+  double* d_shift_part = nullptr; size_t cap_shift_part = 0;
+  void shift_rows(const double* mu_host, bool undo) {
+    if (!n_local_) return;
+    double* dmu = ensure(d_mu, cap_mu, nf);
+    HIP_OK(hipMemcpyAsync(dmu, mu_host, nf * sizeof(double), hipMemcpyHostToDevice, stream));
+    const unsigned gx = (unsigned)std::min<uint64_t>((n_local_ / 2 + 255) / 256 + 1, std::max(1, 4 * n_cu));
+    if (undo) k_shift_rows<true><<<dim3(gx, (unsigned)nf), 256, 0, stream>>>(X, ldx, n_local_, dmu);
+    else k_shift_rows<false><<<dim3(gx, (unsigned)nf), 256, 0, stream>>>(X, ldx, n_local_, dmu);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(stream));  // the host μ buffer may go away after return
+  }
+  void unshift_x() {
+    if (xshift_.empty()) return;
+    shift_rows(xshift_.data(), true);
+    xshift_.clear();
+    raw_sums_.clear();
+  }
+  // the μ the kernels must still subtract: always null (see above)
+  const double* resident_mu(const double* mu) {
+    if (mu && !xshift_.empty() && std::memcmp(mu, xshift_.data(), nf * sizeof(double)) == 0) return nullptr;
+    unshift_x();
+    if (mu) {
+      raw_sums_.assign(nf, 0.0);
+      // own buffers: callers may hold d_stats / d_part pointers across this call
+      double* st = ensure(d_shift_sum, cap_shift_sum, nf);
+      local_rowsum(st, d_shift_part, cap_shift_part);
+      HIP_OK(hipMemcpyAsync(raw_sums_.data(), st, nf * sizeof(double), hipMemcpyDeviceToHost, stream));
+      shift_rows(mu, false);
+      xshift_.assign(mu, mu + nf);
+    }
+    return nullptr;
   }
 
   void gram(const double* mu, double* out) override {
@@ -2273,11 +2346,7 @@ struct DeviceCtx : Evaluator {
     const int nfp = 16 * std::max(nb, 1);  // fused pass: K padded to 16·NB (host builds Wp accordingly)
     const bool fused = nb > 0 && nf <= (uint64_t)nfp && !(need_h && nb == 8) &&
                        !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0));
-    double* dmu = nullptr;
-    if (mu) {
-      dmu = ensure(d_mu, cap_mu, std::max<size_t>(nfp, nf));
-      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    }
+    const double* dmu = resident_mu(mu);  // null: X is centred in place
     const bool tiled = !fused && tiled_ok(nc, dens, alpha);
     if (tiled) {
       HIP_OK(hipEventRecord(ev[1], stream));
@@ -2355,11 +2424,7 @@ struct DeviceCtx : Evaluator {
     double* dw = ensure(d_w, cap_w, wt.size());
     HIP_OK(hipEventRecord(ev[0], stream));
     HIP_OK(hipMemcpyAsync(dw, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
-    double* dmu = nullptr;
-    if (mu) {
-      dmu = ensure(d_mu, cap_mu, nf);
-      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    }
+    const double* dmu = resident_mu(mu);  // null: X is centred in place
     const size_t pst = (size_t)ML_NA * 2 * ncp;
     const double* dal = dw + (size_t)2 * nfp * ncp;
     if (ks) {
@@ -2689,11 +2754,7 @@ struct DeviceCtx : Evaluator {
       const size_t total = EvalStats::size(nc, need_h);
       double* st = ensure(d_stats, cap_stats, total);
       HIP_OK(hipEventRecord(ev[0], stream));
-      double* dmu = nullptr;
-      if (mu) {
-        dmu = ensure(d_mu, cap_mu, nf);
-        HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
-      }
+      const double* dmu = resident_mu(mu);  // null: X is centred in place
       HIP_OK(hipEventRecord(ev[1], stream));
       tiled_eval(w, nc, dmu, d.kind, d.alpha, need_h, st, 1);
       HIP_OK(hipEventRecord(ev[2], stream));
@@ -2721,11 +2782,7 @@ struct DeviceCtx : Evaluator {
     double* st = ensure(d_stats, cap_stats, total);
     double* st_rows = st + total - 2 * nc;  // [Σℓ | Σy²] are the last 2·nc entries
     HIP_OK(hipEventRecord(ev[0], stream));
-    double* dmu = nullptr;
-    if (mu) {
-      dmu = ensure(d_mu, cap_mu, std::max<size_t>(nfp, nf));
-      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    }
+    const double* dmu = resident_mu(mu);  // null: X is centred in place
     std::vector<double> wp((size_t)16 * nb * nfp, 0.0);
     for (size_t i = 0; i < nc; ++i)
       for (size_t k = 0; k < nf; ++k) wp[i * nfp + k] = w[i * nf + k];
@@ -2825,11 +2882,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     double* dw = ensure(d_w, cap_w, nc * nf);
     HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    double* dmu = nullptr;
-    if (mu) {
-      dmu = ensure(d_mu, cap_mu, nf);
-      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    }
+    const double* dmu = resident_mu(mu);  // null: X is centred in place
     const uint64_t CH = 1ull << 20;
     double* Y = ensure(d_chunk, cap_chunk, nc * CH);
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
@@ -2854,11 +2907,7 @@ struct DeviceCtx : Evaluator {
     }
     double* dw = ensure(d_w, cap_w, nc * nf);
     HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    double* dmu = nullptr;
-    if (mu) {
-      dmu = ensure(d_mu, cap_mu, nf);
-      HIP_OK(hipMemcpyAsync(dmu, mu, nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    }
+    const double* dmu = resident_mu(mu);  // null: X is centred in place
     const bool mfma_path = nc <= 64;  // larger nc: the VALU tile kernel
     const uint64_t CH = mfma_path ? (1ull << 22) : (1ull << 16);
     // tiles of the upper triangle and the T split (≈ whole rounds of one workgroup per CU)

@@ -26,12 +26,13 @@ for k, c in per.items():
     a = agg[names[k]]
     a["ms"].append(ns / 1e6)
     a["clock_ghz"].append(c["GRBM_GUI_ACTIVE"] / 8 / ns)
-    for key in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES",
-                "SQ_ACTIVE_INST_VALU", "SQ_INSTS_LDS", "SQ_WAIT_INST_ANY"):
-        a[key].append(c.get(key, float("nan")))
+    for key, v in c.items():
+        if key.startswith("SQ_"):
+            a[key].append(v)
 for name, a in agg.items():
     m = {k: sum(v) / len(v) for k, v in a.items()}
-    print(f"{name}: launches={len(a['ms'])} ms={m['ms']:.2f} clock={m['clock_ghz']:.3f} GHz "
-          f"valu/mfma={m['SQ_INSTS_VALU'] / max(m['SQ_INSTS_MFMA'], 1):.2f} "
-          f"mfma_busy/busy={m['SQ_VALU_MFMA_BUSY_CYCLES'] / max(m['SQ_BUSY_CYCLES'], 1):.3f} "
+    extra = ""
+    if "SQ_INSTS_MFMA" in m:
+        extra = f"valu/mfma={m['SQ_INSTS_VALU'] / max(m['SQ_INSTS_MFMA'], 1):.2f} "
+    print(f"{name}: launches={len(a['ms'])} ms={m['ms']:.2f} clock={m['clock_ghz']:.3f} GHz " + extra
           + " ".join(f"{k}={m[k]:.4g}" for k in sorted(m) if k.startswith("SQ_")))
