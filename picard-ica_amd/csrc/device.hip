@@ -865,6 +865,8 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
   }
 }
 
+#include "loss2.inc"
+
 template <int NB, bool NEED_H, int DENS>
 __global__ void __launch_bounds__(FUSED_THREADS, 4)
 k_eval_fromy(const double* __restrict__ ybuf, uint64_t n_local, double alpha, uint64_t bpw, uint64_t n_blocks,
@@ -2682,11 +2684,27 @@ struct DeviceCtx : Evaluator {
     const int nwg = partition(n_blocks, &bpw);
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * S::NCP);
     const size_t lds = (size_t)2 * S::TS * 16 * NB * 16 * sizeof(double);
-    HIP_OK(hipEventRecord(ev[1], stream));
-    if (store) {
+    // NB = 8 on the centred resident X: LDS-DMA staging, two blocks per barrier
+    // (PICARD_LOSS2=0 selects k_eval_loss<8>, for A/B timing)
+    static const bool loss2_on = [] {
+      const char* e = std::getenv("PICARD_LOSS2");
+      return !(e && e[0] == '0');
+    }();
+    if (NB == 8 && dmu == nullptr && loss2_on) {
+      const size_t lds2 = (size_t)2 * 2 * 128 * 16 * sizeof(double);
+      HIP_OK(hipEventRecord(ev[1], stream));
+      if (store)
+        k_eval_loss2<D, true, Q><<<nwg, FUSED_THREADS, lds2, stream>>>(X, ldx, (int)nf, d_w, alpha, bpw, n_blocks, part,
+                                                                      d_ybuf);
+      else
+        k_eval_loss2<D, false, Q><<<nwg, FUSED_THREADS, lds2, stream>>>(X, ldx, (int)nf, d_w, alpha, bpw, n_blocks, part,
+                                                                       nullptr);
+    } else if (store) {
+      HIP_OK(hipEventRecord(ev[1], stream));
       k_eval_loss<NB, D, true, Q><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw,
                                                                     n_blocks, part, d_ybuf);
     } else {
+      HIP_OK(hipEventRecord(ev[1], stream));
       k_eval_loss<NB, D, false, Q><<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha,
                                                                      bpw, n_blocks, part, nullptr);
     }
