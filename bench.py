@@ -189,7 +189,7 @@ def main():
         except Exception:
             pass
     kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2>", 4.0),
-             "loss": ("k_eval_loss", "k_eval_loss<8,tanh,nostore,noY2>", 2.0)}
+             "loss": ("k_eval_loss", "k_eval_loss2<tanh,nostore,noY2>", 2.0)}
     rooflines = []
     for kind, (short, label, c) in kinds.items():
         ms, nl = brk.get(kind, (0.0, 0))
