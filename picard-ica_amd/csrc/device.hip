@@ -28,6 +28,9 @@
 namespace pcamd {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+// LDS-DMA (global_load_lds) operand address spaces
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* gbl_vptr;
 
 enum { DENS_TANH = 0, DENS_EXP = 1, DENS_CUBE = 2, DENS_LINEAR = 3, DENS_NONE = 4 };
 
@@ -247,36 +250,7 @@ __device__ __forceinline__ void exp_tab_load(double* tab) {
 // r = x − m·ln2/32 is one fma (error ≤ |m|·2^-59·e^x ≤ 3e-17 absolute for
 // x ≤ 0, 0 for m = 0); e^r − 1 = r + r²·p(r), p of degree 4 (near-minimax on
 // |r| ≤ ln2/64, mpmath chebyfit: ≤ 2.2e-19 absolute). 15 VALU + 1 LDS read per
-// element against 19 for the table-free degree-11 form.
-// Table-free variant (sc = 2^k, |r| ≤ ln2/2, degree-11 e^r − 1): 19 VALU per
-// element, no LDS read and fewer live registers — for kernels at the edge of
-// their VGPR budget (k_multi_loss2 at nf = 256).
-template <int NW>
-__device__ __forceinline__ void exp_n_poly(const double* x, double* emr, double* sc) {
-  constexpr double SHIFT = 0x1.8p52;
-  double t[NW], r[NW], p[NW];
-#pragma unroll
-  for (int i = 0; i < NW; ++i) t[i] = __builtin_fma(x[i], fm::LOG2E, SHIFT);
-#pragma unroll
-  for (int i = 0; i < NW; ++i) r[i] = __builtin_fma(-(t[i] - SHIFT), fm::LN2, x[i]);
-  constexpr double C[10] = {0x1.af389ecfc4b9cp-26, 0x1.28917c89a43a7p-22, 0x1.71de0db2f6b19p-19,
-                            0x1.a019b9149a41cp-16, 0x1.a01a01a7c2efep-13, 0x1.6c16c17889ef1p-10,
-                            0x1.11111111109b5p-7,  0x1.5555555553d68p-5,  0x1.5555555555556p-3,
-                            0x1.0000000000001p-1};
-#pragma unroll
-  for (int i = 0; i < NW; ++i) p[i] = __builtin_fma(C[0], r[i], C[1]);
-#pragma unroll
-  for (int c = 2; c < 10; ++c)
-#pragma unroll
-    for (int i = 0; i < NW; ++i) p[i] = __builtin_fma(p[i], r[i], C[c]);
-#pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    emr[i] = __builtin_fma(r[i] * r[i], p[i], r[i]);
-    const int k = __double2loint(t[i]);
-    sc[i] = __hiloint2double((k + 1023) << 20, 0);
-  }
-}
-
+// element against 19 for a table-free degree-11 form.
 template <int NW>
 __device__ __forceinline__ void exp_n(const double* x, const double* tab, double* emr, double* sc) {
   constexpr double SHIFT = 0x1.8p52;
@@ -368,7 +342,7 @@ __device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m
 }
 
 // ℓ terms only (line-search tries): identical arithmetic to density_acc4's ℓ part
-template <int DENS, bool NEED_Q, int NW = 4, bool TAB = true>
+template <int DENS, bool NEED_Q, int NW = 4>
 __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a, const double* tab, RowAcc& a) {
   if constexpr (NEED_Q || DENS == DENS_CUBE)  // as density_acc4 (cube's fused pass keeps Σy²)
 #pragma unroll
@@ -379,19 +353,19 @@ __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a,
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) x[i] = fmax(m2a * fabs(y[g + i]), -708.0);
-      if constexpr (TAB) exp_n<NW>(x, tab, emr, sc); else exp_n_poly<NW>(x, emr, sc);
+      exp_n<NW>(x, tab, emr, sc);
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
         const double em = __builtin_fma(sc[i], emr[i], sc[i] - 1.0);
         a.l += fabs(y[g + i]);
         a.p *= 2.0 + em;
       }
-      if constexpr (TAB) __builtin_amdgcn_sched_barrier(0);  // one group's chain live at a time
+      __builtin_amdgcn_sched_barrier(0);  // one group's chain live at a time
     } else if constexpr (DENS == DENS_EXP) {
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) x[i] = fmax(-alpha / 2.0 * (y[g + i] * y[g + i]), -708.0);
-      if constexpr (TAB) exp_n<NW>(x, tab, emr, sc); else exp_n_poly<NW>(x, emr, sc);
+      exp_n<NW>(x, tab, emr, sc);
 #pragma unroll
       for (int i = 0; i < NW; ++i) a.l += __builtin_fma(sc[i], emr[i], sc[i]) - 1.0;
     } else if constexpr (DENS == DENS_CUBE) {
@@ -730,8 +704,8 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 //   waves 0-7  ("Y waves"): Y stage + density of row block w (W fragment in
 //              VGPRs), ψ / y fragments → LDS images;
 //   waves 8-15 ("G waves"): the G tiles of k_eval_fused<8> (GI = 4 × GJ = 2
-//              accumulators in VGPRs) and the X staging (global → registers →
-//              X − μ → LDS, prefetched a full iteration ahead).
+//              accumulators in VGPRs) and the X staging (LDS-DMA of the centred
+//              resident X, issued a full iteration ahead).
 // k_eval_fused<8> holds both roles in every wave (256 VGPRs: 2 waves per SIMD,
 // the barrier and MFMA → VALU latencies exposed); split, each role fits 128
 // VGPRs and a CU runs 4 waves per SIMD. Each role runs its own loop (so the W
@@ -1191,8 +1165,8 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
            const double* __restrict__ WpT, const double* __restrict__ mu, double alpha, uint64_t bpw,
            uint64_t n_blocks, double* __restrict__ partials, int accumulate, double* __restrict__ ybuf,
            double* __restrict__ pbuf, double* __restrict__ dbuf) {
-  constexpr int NFP = 4 * KS, XS = 16 * NFP, PRE = XS / 2 / FUSED_THREADS;
-  static_assert(XS / 2 % FUSED_THREADS == 0, "X block must split evenly over the workgroup");
+  constexpr int NFP = 4 * KS, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave per block
+  static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int nib = ncp / 16;
@@ -1211,50 +1185,28 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint64_t b_last = b_end - 1;
-  int xk[PRE], xt[PRE];
-  double xmu[PRE];
-  const double* xsrc[PRE];
+  // X staged by LDS-DMA (the centred resident X: μ = null; samples past n_in are
+  // the zero padding of X, rows ≥ nf read row 0 against zero W columns): wave w
+  // moves rows [w·NFP/8, (w+1)·NFP/8), 8 rows × 16 samples per instruction
+  (void)mu;
+  const double* src[NU];
 #pragma unroll
-  for (int p = 0; p < PRE; ++p) {
-    const int e = tid + p * FUSED_THREADS;
-    xk[p] = e / 8;
-    xt[p] = 2 * (e % 8);
-    const bool ok = xk[p] < nf;
-    xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
-    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
+  for (int u = 0; u < NU; ++u) {
+    const int xr = wave * (NFP / 8) + 8 * u + (lane >> 3);
+    src[u] = X + (size_t)(xr < nf ? xr : 0) * ldx + 2 * (lane & 7);
   }
-  double2 pre[PRE];
-  auto load_x = [&](uint64_t b) {
+  auto stage = [&](uint64_t b, double* xs) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * 16);
+    for (int u = 0; u < NU; ++u)
+      __builtin_amdgcn_global_load_lds((gbl_vptr)(src[u] + b * 16),
+                                       (lds_vptr)(xs + (wave * (NFP / 8) + 8 * u) * 16), 16, 0, 0);
   };
-  auto store_x = [&](uint64_t b, double* xs) {
-    if (b * 16 + 16 <= n_in) {
-#pragma unroll
-      for (int p = 0; p < PRE; ++p)
-        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
-    } else {
-#pragma unroll
-      for (int p = 0; p < PRE; ++p) {
-        const uint64_t tg = b * 16 + xt[p];
-        double2 v;
-        v.x = tg < n_in ? pre[p].x - xmu[p] : 0.0;
-        v.y = tg + 1 < n_in ? pre[p].y - xmu[p] : 0.0;
-        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = v;
-      }
-    }
-  };
-  // blocks past n_in (the rest of the last 64-sample tile) are loaded clamped and
-  // staged as zeros: their y = ψ = 0 fragments add nothing in phase 2
-  auto clampb = [&](uint64_t b) { return b * 16 < n_in ? b : (n_in ? (n_in - 1) / 16 : 0); };
   if (b_begin < b_end) {
-    load_x(clampb(b_begin));
-    store_x(b_begin, xs0);
+    stage(b_begin, xs0);
     __syncthreads();
     int cur = 0;
     for (uint64_t b = b_begin; b < b_end; ++b) {
-      load_x(clampb(b < b_last ? b + 1 : b_last));
-      __builtin_amdgcn_sched_barrier(0);
+      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
       if (active) {
         d4 yv = d4{0, 0, 0, 0};
         const double* xrow = xs0 + cur * XS + lk * 16 + lr;
@@ -1277,9 +1229,7 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
         }
         if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      store_x(b < b_last ? b + 1 : b_last, xs0 + (cur ^ 1) * XS);
-      __syncthreads();
+      __syncthreads();  // also waits for this wave's LDS-DMA of block b + 1
       cur ^= 1;
     }
   }
@@ -1547,8 +1497,8 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
               const double* __restrict__ WpT, const double* __restrict__ ZpT, const double* __restrict__ mu,
               double alpha, const double* __restrict__ alphas, int na, uint64_t bpw, uint64_t n_blocks,
               double* __restrict__ partials) {
-  constexpr int NFP = 4 * KS, KH = KS / 2, XS = 16 * NFP, PRE = XS / 2 / FUSED_THREADS;
-  static_assert(XS / 2 % FUSED_THREADS == 0, "X block must split evenly over the workgroup");
+  constexpr int NFP = 4 * KS, KH = KS / 2, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave
+  static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int nib = ncp / 16;
@@ -1578,50 +1528,29 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint64_t b_last = b_end - 1;
-  int xk[PRE], xt[PRE];
-  double xmu[PRE];
-  const double* xsrc[PRE];
+  // X staged by LDS-DMA as in k_tiled_yw (centred resident X, μ = null)
+  (void)mu;
+  const double* src[NU];
 #pragma unroll
-  for (int p = 0; p < PRE; ++p) {
-    const int e = tid + p * FUSED_THREADS;
-    xk[p] = e / 8;
-    xt[p] = 2 * (e % 8);
-    const bool ok = xk[p] < nf;
-    xmu[p] = (ok && mu) ? mu[xk[p]] : 0.0;
-    xsrc[p] = X + (size_t)(ok ? xk[p] : 0) * ldx + xt[p];
+  for (int u = 0; u < NU; ++u) {
+    const int xr = wave * (NFP / 8) + 8 * u + (lane >> 3);
+    src[u] = X + (size_t)(xr < nf ? xr : 0) * ldx + 2 * (lane & 7);
   }
-  double2 pre[PRE];
-  auto load_x = [&](uint64_t b) {
+  auto stage = [&](uint64_t b, double* xs) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) pre[p] = *reinterpret_cast<const double2*>(xsrc[p] + b * 16);
-  };
-  auto store_x = [&](uint64_t b, double* xs) {
-    if (b * 16 + 16 <= n_local) {
-#pragma unroll
-      for (int p = 0; p < PRE; ++p)
-        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = double2{pre[p].x - xmu[p], pre[p].y - xmu[p]};
-    } else {
-#pragma unroll
-      for (int p = 0; p < PRE; ++p) {
-        const uint64_t tg = b * 16 + xt[p];
-        double2 v;
-        v.x = tg < n_local ? pre[p].x - xmu[p] : 0.0;
-        v.y = tg + 1 < n_local ? pre[p].y - xmu[p] : 0.0;
-        *reinterpret_cast<double2*>(xs + xk[p] * 16 + xt[p]) = v;
-      }
-    }
+    for (int u = 0; u < NU; ++u)
+      __builtin_amdgcn_global_load_lds((gbl_vptr)(src[u] + b * 16),
+                                       (lds_vptr)(xs + (wave * (NFP / 8) + 8 * u) * 16), 16, 0, 0);
   };
   auto exch = [&](int buf, int half, int yz, int r) -> double* {
     return ex0 + ((((buf * 2 + half) * 4 + rb) * 2 + yz) * 4 + r) * 64 + lane;
   };
   if (b_begin < b_end) {
-    load_x(b_begin);
-    store_x(b_begin, xs0);
+    stage(b_begin, xs0);
     __syncthreads();
     int cur = 0;
     for (uint64_t b = b_begin; b < b_end; ++b) {
-      load_x(b < b_last ? b + 1 : b_last);
-      __builtin_amdgcn_sched_barrier(0);
+      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
       if (active) {  // partial Yᵀ, Zᵀ over this wave's K-half
         d4 ya = d4{0, 0, 0, 0}, za = d4{0, 0, 0, 0};
         const double* xrow = xs0 + cur * XS + (4 * kh * KH + lk) * 16 + lr;
@@ -1637,9 +1566,7 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
           *exch(cur, kh, 1, r) = za[r];
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
-      store_x(b < b_last ? b + 1 : b_last, xs0 + (cur ^ 1) * XS);
-      __syncthreads();
+      __syncthreads();  // exchange visible; this wave's LDS-DMA of block b + 1 landed
       if (active) {  // Y, Z summed in K order (identical in both waves of the pair), then the tries
         d4 yv, zv;
 #pragma unroll
@@ -1653,7 +1580,7 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
             d4 yj;
 #pragma unroll
             for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj[u], zv[r], yv[r]);
-            loss_acc4<DENS, NEED_Q, 1, (KS < 64)>(yj, alpha, m2a, s_exp_tab, racc[u]);  // KS = 64: no table (VGPRs)
+            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, s_exp_tab, racc[u]);
             if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
           }
         }

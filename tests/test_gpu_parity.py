@@ -170,6 +170,29 @@ def test_rowsum_gram_sources(pa, rng):
         assert rel_err(ctx.sources(w, mu), w @ xc) <= TOL
 
 
+@pytest.mark.parametrize("n", [8, 64, 128])
+def test_resident_centring_is_exact(pa, rng, n):
+    """The first pass with a mean μ centres the resident X in place (DeviceCtx::resident_mu):
+    its statistics are bit-identical to a pass over data centred on the host (the same IEEE
+    subtraction), rowsum() still returns the caller's sums, and download() restores X."""
+    x = laplace_mix(rng, n, 4099)
+    mu = x.mean(axis=1)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    d = pa.DensityType.tanh()
+    ctx = ctx_with(pa, x)
+    sums = ctx.rowsum()
+    got = ctx.eval(w, mu, d, False, need_y2=True)
+    ref_ctx = ctx_with(pa, x - mu[:, None])
+    want = ref_ctx.eval(w, None, d, False, need_y2=True)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), k
+    assert np.array_equal(ctx.rowsum(), sums)
+    again = ctx.eval(w, mu, d, False, need_y2=True)  # same μ: no second shift
+    for k in want:
+        assert np.array_equal(again[k], want[k]), k
+    assert rel_err(ctx.download(), x) <= 1e-15
+
+
 def test_moments4(pa, rng):
     n = 6
     x = laplace_mix(rng, n, 3000)
