@@ -222,10 +222,16 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   init_core();
 }
 
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
   ev_->want_y2 = !cfg_.ortho;  // Σy² is read only by the non-orthogonal step / extended loss
+  const double t0 = now_ms();
   ev_->eval(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
+  eval_ms_ += now_ms() - t0;
   ++last_evals_;
   ++total_evals_;
 }
@@ -233,15 +239,19 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
 bool Solver::evaluate_loss(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
   ev_->want_y2 = !cfg_.ortho;
+  const double t0 = now_ms();
   const bool partial =
       ev_->eval_loss(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out, keep_y_);
+  eval_ms_ += now_ms() - t0;
   ++last_evals_;
   ++total_evals_;
   return partial;
 }
 
 void Solver::complete(EvalStats* out) {
+  const double t0 = now_ms();
   ev_->eval_complete(cfg_.density, !cfg_.ortho, out);
+  eval_ms_ += now_ms() - t0;
   ++total_completions_;
 }
 
@@ -389,7 +399,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     Mat transform;
     if (ortho) {
       if (k == 0) {
+        const double tm = now_ms();
         r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
+        map1_ms_ = now_ms() - tm;
         if (tries > 1) {
           if (!ahead_) ahead_.reset(new TransformWorker());
           ahead_->submit(direction, W_, tries);
@@ -473,6 +485,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
 
 bool Solver::step() {
   if (done_) return true;
+  const double step_t0 = now_ms(), eval_t0 = eval_ms_;
   const size_t n = nc_;
   const double t_f = (double)T_;
   const bool ortho = cfg_.ortho != 0;
@@ -577,9 +590,11 @@ bool Solver::step() {
     res.loss = loss_of(res.stats, res.w, signs_, &singular);
   }
   if (trace_) {
-    std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e\n",
+    const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
+    std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
+                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
-                 res.partial ? 1 : 0, slope);
+                 res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_);
   }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;
