@@ -13,6 +13,7 @@
 // the G-stage waves through LDS without any transpose. Per-workgroup partial
 // sums are reduced by k_reduce in a fixed order (bit-reproducible; no atomics).
 #include <hip/hip_runtime.h>
+#include <hip/hip_cooperative_groups.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -1969,6 +1970,8 @@ __device__ __forceinline__ double laplace_of(uint64_t st) {
   return u < 0.5 ? log(2.0 * u) : -log(2.0 * (1.0 - u));
 }
 
+#include "jade_sweeps.inc"
+
 __global__ void k_gen_sources(double* __restrict__ S, uint64_t lds, int nf, uint64_t t_begin, uint64_t cn,
                               uint64_t seed, uint64_t jump_a, uint64_t jump_c) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -2839,6 +2842,60 @@ struct DeviceCtx : Evaluator {
                               hipMemcpyDeviceToHost, stream));
     }
     HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  // JADE sweeps as one cooperative launch (jade_sweeps.inc): the np cumulant
+  // matrices stay in the LDS of ≤ #CU workgroups for the whole run. Only when
+  // they fit (n ≲ 66 on MI355X: np·npos·8 B over 256 CUs) and the device can
+  // co-schedule the grid; otherwise the host runs the sweeps.
+  bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v_out, size_t* sweeps) override {
+    HIP_OK(hipSetDevice(device));
+    if (n < 2 || n > 256) return false;
+    const size_t np = n * (n + 1) / 2, npos = np;
+    const size_t mw = (np + n_cu - 1) / n_cu;
+    const size_t G = (np + mw - 1) / mw;
+    const size_t lds = (npos * mw + 4) * sizeof(double);
+    if (lds > 160 * 1024 || G > (size_t)n_cu || G > (size_t)JS_MAX_WG) return false;
+    int coop = 0;
+    HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
+    if (!coop) return false;
+    HIP_OK(hipFuncSetAttribute((const void*)k_jade_sweeps, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_jade_sweeps, JS_THREADS, lds));
+    if ((size_t)per_cu * n_cu < G) return false;
+    // [G][npos][mw]: workgroup g owns matrices g·mw … g·mw + mw − 1 (zero-padded)
+    std::vector<double> a_wg(G * npos * mw, 0.0);
+    for (size_t gg = 0; gg < G; ++gg)
+      for (size_t ps = 0; ps < npos; ++ps)
+        for (size_t j = 0; j < mw; ++j) {
+          const size_t m = gg * mw + j;
+          if (m < np) a_wg[(gg * npos + ps) * mw + j] = A[ps * np + m];
+        }
+    std::vector<double> eye(n * n, 0.0);
+    for (size_t i = 0; i < n; ++i) eye[i * n + i] = 1.0;
+    double *d_a = nullptr, *d_v = nullptr, *d_g = nullptr;
+    int* d_sw = nullptr;
+    unsigned* d_bar = nullptr;
+    HIP_OK(hipMalloc(&d_a, a_wg.size() * sizeof(double)));
+    HIP_OK(hipMalloc(&d_v, n * n * sizeof(double)));
+    HIP_OK(hipMalloc(&d_g, 2 * G * 3 * sizeof(double)));
+    HIP_OK(hipMalloc(&d_sw, sizeof(int)));
+    HIP_OK(hipMalloc(&d_bar, sizeof(unsigned)));
+    HIP_OK(hipMemsetAsync(d_bar, 0, sizeof(unsigned), stream));
+    HIP_OK(hipMemcpyAsync(d_a, a_wg.data(), a_wg.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_v, eye.data(), n * n * sizeof(double), hipMemcpyHostToDevice, stream));
+    int n_i = (int)n, npos_i = (int)npos, mw_i = (int)mw, it_i = (int)std::min<size_t>(max_iter, 1u << 30);
+    double tol_d = tol;
+    void* args[] = {&d_a, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_bar, &d_sw};
+    HIP_OK(hipLaunchCooperativeKernel((const void*)k_jade_sweeps, dim3((unsigned)G), dim3(JS_THREADS), args,
+                                      (unsigned)lds, stream));
+    int sw = 0;
+    HIP_OK(hipMemcpyAsync(v_out, d_v, n * n * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(&sw, d_sw, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    for (void* pf : {(void*)d_a, (void*)d_v, (void*)d_g, (void*)d_sw, (void*)d_bar}) (void)hipFree(pf);
+    *sweeps = (size_t)sw;
+    return true;
   }
 
   void moments4(const double* w, size_t nc, const double* mu, double* out) override {

@@ -80,6 +80,14 @@ class Evaluator {
     (void)w; (void)z; (void)nc; (void)mu; (void)d; (void)alphas; (void)na; (void)ll_out; (void)y2_out;
     return false;
   }
+  // JADE sweeps (jade.rs:37-69) on the np = n(n+1)/2 cumulant matrices A, packed
+  // position-major (A[pos(k,l)·np + m], k ≤ l, pos as in Solver::jade). On success
+  // v (n×n, row-major) holds the accumulated rotation V and *sweeps the sweeps
+  // run; false = not supported here (the host runs them).
+  virtual bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v, size_t* sweeps) {
+    (void)A; (void)n; (void)max_iter; (void)tol; (void)v; (void)sweeps;
+    return false;
+  }
   // eval_complete into a raw packed stats buffer (C ABI)
   virtual void eval_complete_into(pc_density d, bool need_h, double* stats) {
     (void)d; (void)need_h; (void)stats;

@@ -725,6 +725,24 @@ Mat Solver::jade(size_t max_iter, double tol) {
   }
   if (cfg_.verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
   Mat v = Mat::eye(n);
+  // PICARD_DEVICE_JADE=1: the sweeps as one cooperative device launch
+  // (DeviceCtx::jade_sweeps). Not the default: each of the 100,800 sequential
+  // Givens pairs of C5 (50 sweeps × 2016) needs a grid barrier across the 8 XCDs
+  // (agent-scope release/acquire through the memory side, ≈12 µs per pair: 1.24 s),
+  // while 8 host threads on one CCD sync through L3 (≈10 µs per pair: 1.0 s).
+  size_t dev_sweeps = 0;
+  if (std::getenv("PICARD_DEVICE_JADE") && ev_->jade_sweeps(A.data(), n, max_iter, tol, v.data(), &dev_sweeps)) {
+    if (cfg_.verbose && dev_sweeps < max_iter) std::printf("JADE converged after %zu iterations\n", dev_sweeps);
+    if (std::getenv("PICARD_TRACE")) {
+      const auto tj2 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "[picard-trace] jade: moments %.3f s, device sweeps %.3f s (%zu sweeps)\n",
+                   std::chrono::duration<double>(tj1 - tj0).count(), std::chrono::duration<double>(tj2 - tj1).count(),
+                   dev_sweeps);
+    }
+    Mat w;
+    if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
+    return w;
+  }
   // Sweeps in the reference's cyclic (p, q) order. The np matrices are split
   // into NCH fixed chunks; each thread rotates its chunks and forms their
   // partial g-sums for the NEXT pair, and every thread sums the partials in

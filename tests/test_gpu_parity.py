@@ -259,6 +259,19 @@ def test_fit_variants_vs_oracle(pa, po, c1_data, kw):
     assert np.max(np.abs(fw - fwo)) <= 1e-5 * np.max(np.abs(fwo))
 
 
+@pytest.mark.parametrize("jade_it", [1, 3])
+def test_jade_device_sweeps_match_host(pa, c1_data, monkeypatch, jade_it):
+    """The Jacobi sweeps as one cooperative device launch (PICARD_DEVICE_JADE=1,
+    DeviceCtx::jade_sweeps) against the host sweeps on the same cumulant matrices: the
+    angles differ only by summation order, so after a few sweeps they agree to ~1e-12."""
+    x, s, a = c1_data
+    cfg = dict(jade_it=jade_it, max_iter=1, w_init=np.eye(8))
+    host = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg)).full_unmixing()
+    monkeypatch.setenv("PICARD_DEVICE_JADE", "1")
+    dev = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg)).full_unmixing()
+    assert np.max(np.abs(dev - host)) <= 1e-9 * np.max(np.abs(host))
+
+
 def test_jade_long_run_properties(pa, c1_data):
     """jade.rs:22-72 as written never reaches its 1e-6 angle tolerance on this data:
     every sweep rotates by ~0.75 rad and a 1e-15 relative perturbation of the input
