@@ -25,6 +25,7 @@
  *                             G_raw = ψ·Yᵀ [, H_raw = ψ′·(Y∘Y)ᵀ], Σψ′, Σℓ, Σy²
  *   pc_ctx_rowsum / pc_ctx_gram   centering and the whitening Gram X·Xᵀ
  *   pc_ctx_sources            Y = W·(X−μ) materialised (PicardResult.sources)
+ *   pc_ctx_moments4 / pc_ctx_jade   the JADE warm start (src/jade.rs:22-197)
  *
  * Conventions: every matrix is row-major, contiguous, float64. Rows are
  * features/components, columns are samples (src/solver.rs:29,40). Inputs
@@ -125,7 +126,13 @@ typedef struct pc_ctx pc_ctx;
 int pc_rccl_unique_id(char id_out[128]);
 
 /* Each rank owns the samples [t0, t0 + n_local) of a global matrix with
- * n_total samples (contiguous T blocks). */
+ * n_total samples (contiguous T blocks). With world_size > 1 and
+ * rccl_id == NULL the context is a DETACHED shard: no communicator is created,
+ * every pc_ctx_* statistic is this shard's partial sum (per-sample constants
+ * included, counted over its own n_local samples) and the caller adds the
+ * shards up — e.g. one process driving several shards through
+ * pc_fit_with_evaluator. pc_solver_create refuses a detached shard
+ * (PC_ERR_INVALID_CONFIG). */
 int pc_ctx_create(int32_t device, int32_t rank, int32_t world_size, const char* rccl_id /* or NULL */,
                   pc_ctx** out, char* err, size_t errlen);
 void pc_ctx_destroy(pc_ctx* ctx);
@@ -137,7 +144,11 @@ int pc_ctx_load(pc_ctx* ctx, const double* x_shard, uint64_t n_features, uint64_
  * mixing matrix A (n_features²) is written to a_out when not NULL */
 int pc_ctx_generate(pc_ctx* ctx, uint64_t n_features, uint64_t n_total, uint64_t seed,
                     double* a_out, char* err, size_t errlen);
-/* copy this rank's shard back to the host (n_features × n_local) */
+/* copy this rank's shard back to the host (n_features × n_local). The passes
+ * centre X in place (the first call with a mean μ subtracts it from the
+ * resident shard; a call with another μ, or download, adds it back), so after
+ * a fit with centering the downloaded data equal the loaded data only up to
+ * rounding: (x − μ) + μ may differ from x in the last bit. */
 int pc_ctx_download(pc_ctx* ctx, double* x_shard_out);
 uint64_t pc_ctx_n_local(const pc_ctx* ctx);
 uint64_t pc_ctx_t0(const pc_ctx* ctx);
@@ -186,6 +197,20 @@ int pc_ctx_sources(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, 
 int pc_ctx_moments4(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, double* out,
                     char* err, size_t errlen);
 
+/* The JADE warm start (src/jade.rs:22-72, caller solver.rs:124-128) on
+ * Y = W·(X−μ) (W: nc × n_features, normally the whitening K): the fourth-moment
+ * pass on the device (pc_ctx_moments4), the nc(nc+1)/2 cumulant matrices
+ * (jade.rs:78-131), up to max_iter Jacobi sweeps in the reference's cyclic
+ * (p, q) order (jade.rs:37-69) with the angle tolerance tol, and
+ * w_out = sym_decorrelation(V) (nc × nc, jade.rs:69). `where` places the
+ * sweeps: PC_JADE_AUTO (host), PC_JADE_DEVICE (one cooperative device launch;
+ * PC_ERR_COMPUTATION if the shape does not fit it) or PC_JADE_HOST.
+ * sweeps_out (or NULL): [0] sweeps run, [1] 1 if the tolerance was met,
+ * [2] 1 if the sweeps ran on the device. */
+enum { PC_JADE_AUTO = 0, PC_JADE_DEVICE = 1, PC_JADE_HOST = 2 };
+int pc_ctx_jade(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, uint64_t max_iter, double tol,
+                int32_t where, double* w_out, uint64_t sweeps_out[3], char* err, size_t errlen);
+
 /* Stepping solver over a context: pc_fit's pipeline (solver.rs:45-189) split
  * so that a caller can time individual Picard iterations (core.rs:211-391).
  * pc_solver_step runs ONE iteration; *done becomes 1 on convergence or when
@@ -212,6 +237,11 @@ typedef struct {
               uint32_t flags, double* stats);
   int (*sources)(void* user, const double* w, uint64_t nc, const double* mu, double* out);
   int (*moments4)(void* user, const double* w, uint64_t nc, const double* mu, double* out);
+  /* optional (NULL: every non-orthogonal line-search try is a full eval):
+   * pc_ctx_eval_loss_multi's contract */
+  int (*eval_loss_multi)(void* user, const double* w, const double* z, uint64_t nc, const double* mu,
+                         pc_density density, const double* alphas, uint64_t n_alpha, double* ll_out,
+                         double* y2_out);
 } pc_host_evaluator;
 int pc_fit_with_evaluator(const pc_host_evaluator* ev, const pc_config* cfg, pc_result* out,
                           char* err, size_t errlen);

@@ -544,6 +544,61 @@ def jade(x: np.ndarray, max_iter: int, tol: float = 1e-6, verbose: bool = False)
     return sym_decorrelation(v)
 
 
+def jade_sweeps_batched(mats: np.ndarray, max_iter: int, tol: float = 1e-6, max_pairs: Optional[int] = None):
+    """jade.rs:37-69 with the matrix loop of compute_givens_rotation (jade.rs:137-167)
+    vectorised over the stacked cumulant matrices ``mats`` [np, n, n]: the same
+    cyclic (p, q) order, the same b = v_pᵀ M v_q forms recomputed from V for
+    every pair, the same angle formula (jade.rs:172-182) and rotation of V
+    (jade.rs:188-197). Only the order of the g-sums over matrices differs
+    (numpy's). ``max_pairs`` stops after that many Givens pairs in all (a test
+    hook: the sweeps amplify rounding, so parity is checked on prefixes).
+    Returns (V, sweeps run, tolerance met) — before sym_decorrelation."""
+    npm, n, _ = mats.shape
+    flat = np.ascontiguousarray(mats).reshape(npm * n, n)
+    v = np.eye(n)
+    it = 0
+    converged = False
+    done = 0
+    while it < max_iter and not converged:
+        max_theta = 0.0
+        for p in range(n):
+            for q in range(p + 1, n):
+                if max_pairs is not None and done >= max_pairs:
+                    return v, it, False
+                done += 1
+                mv = (flat @ v[:, [p, q]]).reshape(npm, n, 2)  # M v_p, M v_q for every M
+                b00 = mv[:, :, 0] @ v[:, p]
+                b01 = mv[:, :, 1] @ v[:, p]   # v_pᵀ M v_q
+                b10 = mv[:, :, 0] @ v[:, q]   # v_qᵀ M v_p
+                b11 = mv[:, :, 1] @ v[:, q]
+                h_pq = b01 + b10
+                h_d = b00 - b11
+                g00, g01, g11 = float(h_pq @ h_pq), float(h_pq @ h_d), float(h_d @ h_d)
+                diff = g11 - g00
+                angle = 0.0 if (abs(g01) < 1e-15 and abs(diff) < 1e-15) else 0.25 * math.atan2(2.0 * g01, diff)
+                max_theta = max(max_theta, abs(angle))
+                apply_givens_rotation(v, math.cos(angle), math.sin(angle), p, q)
+        it += 1
+        converged = max_theta < tol
+    return v, it, converged
+
+
+def cumulants_from_moments(m4: np.ndarray, n: int, t: float) -> np.ndarray:
+    """jade.rs:101-126 from the pair-product moment matrix m4 = Σ_t z zᵀ, z = (y_i y_j)_{i≤j}
+    (what pc_ctx_moments4 returns): Q_ij[k, l] = E[y_i y_j y_k y_l] − δ_ij δ_kl − δ_ik δ_jl
+    − δ_il δ_jk, symmetrised; stacked [n(n+1)/2, n, n] in the reference's (i ≤ j) order."""
+    pairs = [(i, j) for i in range(n) for j in range(i, n)]
+    pidx = np.zeros((n, n), dtype=np.int64)
+    for a, (i, j) in enumerate(pairs):
+        pidx[i, j] = pidx[j, i] = a
+    eye = np.eye(n)
+    out = np.empty((len(pairs), n, n))
+    for a, (i, j) in enumerate(pairs):
+        q = m4[a][pidx] / t - eye[i, j] * eye - np.outer(eye[i], eye[j]) - np.outer(eye[j], eye[i])
+        out[a] = (q + q.T) / 2.0
+    return out
+
+
 def compute_cumulant_matrices(x: np.ndarray) -> List[np.ndarray]:
     """jade.rs:78-131 (the n×n×T ``xx`` tensor is contracted without materialising it)."""
     n, t = x.shape

@@ -118,13 +118,16 @@ SourcesFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_uint64, 
                         C.POINTER(C.c_double))
 Moments4Fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_uint64, C.POINTER(C.c_double),
                          C.POINTER(C.c_double))
+MultiFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64,
+                      C.POINTER(C.c_double), _Density, C.POINTER(C.c_double), C.c_uint64, C.POINTER(C.c_double),
+                      C.POINTER(C.c_double))
 
 
 class _HostEvaluator(C.Structure):
     _fields_ = [
         ("user", C.c_void_p), ("n_features", C.c_uint64), ("n_samples", C.c_uint64),
         ("rowsum", RowsumFn), ("gram", GramFn), ("eval", EvalFn), ("sources", SourcesFn),
-        ("moments4", Moments4Fn),
+        ("moments4", Moments4Fn), ("eval_loss_multi", MultiFn),
     ]
 
 
@@ -165,6 +168,7 @@ def _load():
         "pc_ctx_gram": (C.c_int, [vp, d, d, cp, sz]),
         "pc_ctx_sources": (C.c_int, [vp, d, u64, d, d, cp, sz]),
         "pc_ctx_moments4": (C.c_int, [vp, d, u64, d, d, cp, sz]),
+        "pc_ctx_jade": (C.c_int, [vp, d, u64, d, u64, C.c_double, i32, d, P(u64), cp, sz]),
         "pc_ctx_last_timing": (None, [vp, d, d]),
         "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
         "pc_device_synchronize": (C.c_int, [i32]),
@@ -192,7 +196,7 @@ EXPORTED = [
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
-    "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 
@@ -619,6 +623,19 @@ class DeviceContext:
                                   _ptr(out), err, len(err)), err)
         return out
 
+    def jade(self, w, mu=None, max_iter: int = 50, tol: float = 1e-6, where: str = "auto"):
+        """pc_ctx_jade: the JADE warm start (jade.rs:22-72) on Y = w·(X − μ).
+        Returns (sym_decorrelation(V), sweeps run, tolerance met, sweeps ran on the device)."""
+        w = _c64(w)
+        nc = w.shape[0]
+        mu_a = _c64(mu) if mu is not None else None
+        out = np.empty((nc, nc))
+        info = (C.c_uint64 * 3)()
+        err = _errbuf()
+        _raise(lib.pc_ctx_jade(self.h, _ptr(w), nc, _ptr(mu_a) if mu_a is not None else None, max_iter, tol,
+                               {"auto": 0, "device": 1, "host": 2}[where], _ptr(out), info, err, len(err)), err)
+        return out, int(info[0]), bool(info[1]), bool(info[2])
+
     def moments4(self, w, mu=None) -> np.ndarray:
         w = _c64(w)
         nc = w.shape[0]
@@ -677,11 +694,13 @@ class Solver:
 
 
 def fit_with_host_evaluator(n_features: int, n_samples: int, config: PicardConfig, *, rowsum, gram, eval,
-                            sources, moments4=None) -> PicardResult:
+                            sources, moments4=None, eval_loss_multi=None) -> PicardResult:
     """Run the host driver over Python callbacks (pc_fit_with_evaluator).
 
-    Test hook for the host logic on machines without a GPU; the callbacks get
-    numpy arrays and must fill ``out`` in place (see pc_host_evaluator)."""
+    Test hook for the host logic on machines without a GPU, or over detached
+    shard contexts on one GPU; the callbacks get numpy arrays and return them
+    (see pc_host_evaluator). ``eval_loss_multi(w, z, alphas, mu, density)``
+    returns (Σℓ, Σy²), each [n_alpha, nc]."""
     def _rs(user, out):
         o = np.ctypeslib.as_array(out, shape=(n_features,))
         o[:] = rowsum()
@@ -722,8 +741,19 @@ def fit_with_host_evaluator(n_features: int, n_samples: int, config: PicardConfi
         o[:] = np.asarray(moments4(W, m)).reshape(-1)
         return 0
 
+    def _multi(user, w, z, nc, mu, dens, al, na, ll_out, y2_out):
+        W = np.ctypeslib.as_array(w, shape=(nc * n_features,)).reshape(nc, n_features).copy()
+        Z = np.ctypeslib.as_array(z, shape=(nc * n_features,)).reshape(nc, n_features).copy()
+        m = np.ctypeslib.as_array(mu, shape=(n_features,)).copy() if mu else None
+        a = np.ctypeslib.as_array(al, shape=(na,)).copy()
+        ll, y2 = eval_loss_multi(W, Z, a, m, DensityType(dens.kind, dens.alpha))
+        np.ctypeslib.as_array(ll_out, shape=(na * nc,))[:] = np.asarray(ll).reshape(-1)
+        np.ctypeslib.as_array(y2_out, shape=(na * nc,))[:] = np.asarray(y2).reshape(-1)
+        return 0
+
     cbs = (RowsumFn(_rs), GramFn(_gram), EvalFn(_eval), SourcesFn(_src),
-           Moments4Fn(_m4) if moments4 is not None else Moments4Fn())
+           Moments4Fn(_m4) if moments4 is not None else Moments4Fn(),
+           MultiFn(_multi) if eval_loss_multi is not None else MultiFn())
     ev = _HostEvaluator(None, n_features, n_samples, *cbs)
     c, _keep = config._c()
     r = _Result()

@@ -83,6 +83,12 @@ struct CallbackEvaluator : Evaluator {
     if (!cb.moments4) throw computation_error("moments4 callback missing");
     chk(cb.moments4(cb.user, w, nc, mu, out), "moments4");
   }
+  bool eval_loss_multi(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
+                       const double* alphas, int na, double* ll_out, double* y2_out) override {
+    if (!cb.eval_loss_multi) return false;
+    chk(cb.eval_loss_multi(cb.user, w, z, nc, mu, d, alphas, (uint64_t)na, ll_out, y2_out), "eval_loss_multi");
+    return true;
+  }
 };
 
 Mat full_unmixing_of(const pc_result* r) {
@@ -380,12 +386,35 @@ int pc_device_synchronize(int32_t device) {
   }
 }
 
+int pc_ctx_jade(pc_ctx* c, const double* w, uint64_t nc, const double* mu, uint64_t max_iter, double tol,
+                int32_t where, double* w_out, uint64_t sweeps_out[3], char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    const uint64_t nf = c->ev->n_features();
+    if (nc == 0 || nc > nf) throw invalid_dimensions("n_components must be in 1..=n_features");
+    if (where < PC_JADE_AUTO || where > PC_JADE_HOST) throw invalid_config("where", "unknown sweep placement");
+    Mat base(nc, nf);
+    std::memcpy(base.data(), w, nc * nf * sizeof(double));
+    JadeInfo info;
+    Mat r = jade_warm_start(c->ev.get(), base, nc, mu, (double)c->ev->n_samples(), max_iter, tol, false, where,
+                            &info);
+    std::memcpy(w_out, r.data(), nc * nc * sizeof(double));
+    if (sweeps_out) {
+      sweeps_out[0] = info.sweeps;
+      sweeps_out[1] = info.converged ? 1 : 0;
+      sweeps_out[2] = info.on_device ? 1 : 0;
+    }
+  });
+}
+
 int pc_solver_create(pc_ctx* c, const pc_config* cfg, pc_solver** out, char* err, size_t errlen) {
   *out = nullptr;
   return guarded(err, errlen, [&] {
     char e2[512];
     int rc = pc_config_validate(cfg, e2, sizeof e2);
     if (rc) throw PicardError(rc, e2);
+    if (c->ev->partial_sums())
+      throw invalid_config("ctx", "a detached shard context (world_size > 1 without an RCCL id) returns partial "
+                                  "sums; drive the shards with pc_fit_with_evaluator");
     auto* s = new pc_solver;
     try {
       s->s.reset(new Solver(c->ev.get(), *cfg));

@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +28,7 @@
 #include "evaluator.hpp"
 
 namespace pcamd {
+size_t jade_max_pairs();  // host_solver.cpp (PICARD_JADE_MAX_PAIRS test hook)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 // LDS-DMA (global_load_lds) operand address spaces
@@ -2016,8 +2018,9 @@ struct DeviceCtx : Evaluator {
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
     n_cu = prop.multiProcessorCount;
-    if (world > 1) {
-      if (!uid) throw computation_error("world_size > 1 needs an RCCL unique id");
+    // world > 1 without an RCCL id: a detached shard (no communicator; every
+    // statistic is this shard's partial sum and the caller adds them up)
+    if (world > 1 && uid) {
       ncclUniqueId id;
       std::memcpy(&id, uid, sizeof id);
       RCCL_OK(ncclCommInitRank(&comm, world, id, rank));
@@ -2035,6 +2038,7 @@ struct DeviceCtx : Evaluator {
   uint64_t n_features() const override { return nf; }
   uint64_t n_samples() const override { return n_total; }
   uint64_t n_local() const override { return n_local_; }
+  bool partial_sums() const override { return world > 1 && !comm; }
 
   double* ensure(double*& p, size_t& cap, size_t n) {
     if (n > cap) {
@@ -2113,7 +2117,7 @@ struct DeviceCtx : Evaluator {
   }
 
   void allreduce(double* d, size_t n) {
-    if (world > 1) RCCL_OK(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm, stream));
+    if (comm) RCCL_OK(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm, stream));
   }
 
   // this shard's row sums of the resident X into st (device), no all-reduce;
@@ -2848,7 +2852,7 @@ struct DeviceCtx : Evaluator {
   // matrices stay in the LDS of ≤ #CU workgroups for the whole run. Only when
   // they fit (n ≲ 66 on MI355X: np·npos·8 B over 256 CUs) and the device can
   // co-schedule the grid; otherwise the host runs the sweeps.
-  bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v_out, size_t* sweeps) override {
+  bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v_out, JadeSweepLog* log) override {
     HIP_OK(hipSetDevice(device));
     if (n < 2 || n > 256) return false;
     const size_t np = n * (n + 1) / 2, npos = np;
@@ -2879,22 +2883,34 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMalloc(&d_a, a_wg.size() * sizeof(double)));
     HIP_OK(hipMalloc(&d_v, n * n * sizeof(double)));
     HIP_OK(hipMalloc(&d_g, 2 * G * 3 * sizeof(double)));
-    HIP_OK(hipMalloc(&d_sw, sizeof(int)));
+    HIP_OK(hipMalloc(&d_sw, 2 * sizeof(int)));
+    const int theta_cap = (int)std::min<size_t>(max_iter / 10, 1u << 16);
+    double* d_th = nullptr;
+    HIP_OK(hipMalloc(&d_th, (theta_cap + 1) * sizeof(double)));
     HIP_OK(hipMalloc(&d_bar, sizeof(unsigned)));
-    HIP_OK(hipMemsetAsync(d_bar, 0, sizeof(unsigned), stream));
+    // the arrival counter starts at bar0 (0; PICARD_JADE_BAR_BASE presets it, e.g.
+    // just below 2^32, so a test can make the barrier targets wrap)
+    unsigned bar0 = 0;
+    if (const char* e = std::getenv("PICARD_JADE_BAR_BASE")) bar0 = (unsigned)std::strtoul(e, nullptr, 0);
+    long long max_pairs = (long long)std::min<size_t>(jade_max_pairs(), (size_t)LLONG_MAX);
+    HIP_OK(hipMemcpyAsync(d_bar, &bar0, sizeof(unsigned), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(d_a, a_wg.data(), a_wg.size() * sizeof(double), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(d_v, eye.data(), n * n * sizeof(double), hipMemcpyHostToDevice, stream));
     int n_i = (int)n, npos_i = (int)npos, mw_i = (int)mw, it_i = (int)std::min<size_t>(max_iter, 1u << 30);
     double tol_d = tol;
-    void* args[] = {&d_a, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_bar, &d_sw};
+    void* args[] = {&d_a, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_bar, &d_sw, &d_th, (void*)&theta_cap, &bar0, &max_pairs};
     HIP_OK(hipLaunchCooperativeKernel((const void*)k_jade_sweeps, dim3((unsigned)G), dim3(JS_THREADS), args,
                                       (unsigned)lds, stream));
-    int sw = 0;
+    int sw[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(v_out, d_v, n * n * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipMemcpyAsync(&sw, d_sw, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(sw, d_sw, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
-    for (void* pf : {(void*)d_a, (void*)d_v, (void*)d_g, (void*)d_sw, (void*)d_bar}) (void)hipFree(pf);
-    *sweeps = (size_t)sw;
+    log->sweeps = (size_t)sw[0];
+    log->converged = sw[1] != 0;
+    log->theta10.assign(std::min<size_t>(log->sweeps / 10, (size_t)theta_cap), 0.0);
+    if (!log->theta10.empty())
+      HIP_OK(hipMemcpy(log->theta10.data(), d_th, log->theta10.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (void* pf : {(void*)d_a, (void*)d_v, (void*)d_g, (void*)d_sw, (void*)d_bar, (void*)d_th}) (void)hipFree(pf);
     return true;
   }
 

@@ -44,6 +44,12 @@ struct EvalStats {
   static size_t size(size_t nc, bool h) { return (h ? 2 : 1) * nc * nc + 3 * nc; }
 };
 
+struct JadeSweepLog {
+  size_t sweeps = 0;
+  bool converged = false;
+  std::vector<double> theta10;  // max |θ| of sweeps 10, 20, …
+};
+
 class Evaluator {
  public:
   virtual ~Evaluator() = default;
@@ -53,6 +59,9 @@ class Evaluator {
   bool want_y2 = true;
   virtual uint64_t n_features() const = 0;
   virtual uint64_t n_samples() const = 0;  // global T over all ranks
+  // true for a detached shard (world > 1, no communicator): every statistic is
+  // this shard's partial sum, so the host driver cannot run on it alone
+  virtual bool partial_sums() const { return false; }
   virtual void rowsum(double* out) = 0;
   virtual void gram(const double* mu, double* out) = 0;
   virtual void eval(const double* w, size_t nc, const double* mu, pc_density d, bool need_h,
@@ -81,11 +90,13 @@ class Evaluator {
     return false;
   }
   // JADE sweeps (jade.rs:37-69) on the np = n(n+1)/2 cumulant matrices A, packed
-  // position-major (A[pos(k,l)·np + m], k ≤ l, pos as in Solver::jade). On success
-  // v (n×n, row-major) holds the accumulated rotation V and *sweeps the sweeps
-  // run; false = not supported here (the host runs them).
-  virtual bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v, size_t* sweeps) {
-    (void)A; (void)n; (void)max_iter; (void)tol; (void)v; (void)sweeps;
+  // position-major (A[pos(k,l)·np + m], k ≤ l, pos as in jade_warm_start). On
+  // success v (n×n, row-major) holds the accumulated rotation V and *log the
+  // sweeps run, whether the angle tolerance was met, and the max angle of
+  // every 10th sweep (the verbose lines of jade.rs:57-66); false = not
+  // supported here (the host runs them).
+  virtual bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v, JadeSweepLog* log) {
+    (void)A; (void)n; (void)max_iter; (void)tol; (void)v; (void)log;
     return false;
   }
   // eval_complete into a raw packed stats buffer (C ABI)

@@ -683,13 +683,29 @@ Mat Solver::ica_par(const Mat& w_init) {
 // pass (jade.rs:78-131) and the Jacobi sweeps on rotated copies VᵀMV kept
 // up to date per Givens rotation (same angles as jade.rs:137-185).
 Mat Solver::jade(size_t max_iter, double tol) {
-  const size_t n = nc_;
+  static const int where = std::getenv("PICARD_DEVICE_JADE") ? JADE_SWEEPS_AUTO_DEVICE : JADE_SWEEPS_AUTO;
+  JadeInfo info;
+  Mat w = jade_warm_start(ev_, has_k_ ? K_ : Mat::eye(nf_), nc_, has_mu_ ? mu_.data() : nullptr, (double)T_,
+                          max_iter, tol, cfg_.verbose, where, &info);
+  if (trace_ || std::getenv("PICARD_TRACE"))
+    std::fprintf(stderr, "[picard-trace] jade: moments %.3f s, %s sweeps %.3f s (%zu sweeps)\n", info.moments_s,
+                 info.on_device ? "device" : "host", info.sweeps_s, info.sweeps);
+  return w;
+}
+
+size_t jade_max_pairs() {
+  const char* e = std::getenv("PICARD_JADE_MAX_PAIRS");
+  return e ? (size_t)std::strtoull(e, nullptr, 0) : SIZE_MAX;
+}
+
+Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, double T, size_t max_iter,
+                    double tol, bool verbose, int where, JadeInfo* info) {
+  *info = JadeInfo();
   if (n < 2) return Mat::eye(n);
   const size_t np = n * (n + 1) / 2;
   std::vector<double> m4(np * np);
-  Mat base = has_k_ ? K_ : Mat::eye(nf_);
   const auto tj0 = std::chrono::steady_clock::now();
-  ev_->moments4(base.data(), n, has_mu_ ? mu_.data() : nullptr, m4.data());
+  ev->moments4(base.data(), n, mu, m4.data());
   const auto tj1 = std::chrono::steady_clock::now();
   std::vector<size_t> pidx(n * n);
   {
@@ -697,7 +713,7 @@ Mat Solver::jade(size_t max_iter, double tol) {
     for (size_t i = 0; i < n; ++i)
       for (size_t j = i; j < n; ++j) { pidx[i * n + j] = pidx[j * n + i] = q++; }
   }
-  const double t = (double)T_;
+  const double t = T;
   // Cumulant matrices Q_ij (jade.rs:101-126), symmetrised, stored packed by
   // position: A[pos(k,l)][m] for k ≤ l, matrix index m innermost, so a Givens
   // step on (p, q) streams 2n contiguous rows of length np and the g-sums of
@@ -723,25 +739,28 @@ Mat Solver::jade(size_t max_iter, double tol) {
           for (size_t l = k; l < n; ++l) A[pos(k, l) * np + m] = (q(k, l) + q(l, k)) / 2.0;
       }
   }
-  if (cfg_.verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
+  if (verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
   Mat v = Mat::eye(n);
-  // PICARD_DEVICE_JADE=1: the sweeps as one cooperative device launch
-  // (DeviceCtx::jade_sweeps). Not the default: each of the 100,800 sequential
-  // Givens pairs of C5 (50 sweeps × 2016) needs a grid barrier across the 8 XCDs
-  // (agent-scope release/acquire through the memory side, ≈12 µs per pair: 1.24 s),
-  // while 8 host threads on one CCD sync through L3 (≈10 µs per pair: 1.0 s).
-  size_t dev_sweeps = 0;
-  if (std::getenv("PICARD_DEVICE_JADE") && ev_->jade_sweeps(A.data(), n, max_iter, tol, v.data(), &dev_sweeps)) {
-    if (cfg_.verbose && dev_sweeps < max_iter) std::printf("JADE converged after %zu iterations\n", dev_sweeps);
-    if (std::getenv("PICARD_TRACE")) {
-      const auto tj2 = std::chrono::steady_clock::now();
-      std::fprintf(stderr, "[picard-trace] jade: moments %.3f s, device sweeps %.3f s (%zu sweeps)\n",
-                   std::chrono::duration<double>(tj1 - tj0).count(), std::chrono::duration<double>(tj2 - tj1).count(),
-                   dev_sweeps);
+  info->moments_s = std::chrono::duration<double>(tj1 - tj0).count();
+  // The sweeps as one cooperative device launch (DeviceCtx::jade_sweeps) where
+  // asked for and supported; the host sweeps otherwise.
+  if (where == JADE_SWEEPS_DEVICE || where == JADE_SWEEPS_AUTO_DEVICE) {
+    JadeSweepLog log;
+    if (ev->jade_sweeps(A.data(), n, max_iter, tol, v.data(), &log)) {
+      if (verbose) {  // jade.rs:57-66
+        for (size_t k = 0; k < log.theta10.size(); ++k)
+          std::printf("JADE iteration %zu: max angle = %s\n", 10 * (k + 1), rust_e4(log.theta10[k]).c_str());
+        if (log.converged) std::printf("JADE converged after %zu iterations\n", log.sweeps);
+      }
+      info->sweeps = log.sweeps;
+      info->converged = log.converged;
+      info->on_device = true;
+      info->sweeps_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tj1).count();
+      Mat w;
+      if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
+      return w;
     }
-    Mat w;
-    if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
-    return w;
+    if (where == JADE_SWEEPS_DEVICE) throw computation_error("device JADE sweeps not supported for this shape");
   }
   // Sweeps in the reference's cyclic (p, q) order. The np matrices are split
   // into NCH fixed chunks; each thread rotates its chunks and forms their
@@ -762,6 +781,10 @@ Mat Solver::jade(size_t max_iter, double tol) {
   };
   size_t sweeps_done = 0;
   bool converged = false;
+  // PICARD_JADE_MAX_PAIRS (test hook): stop after that many Givens pairs in all.
+  // The sweeps amplify rounding exponentially, so parity
+  // with the reference's literal form is checked on prefixes of a sweep.
+  const size_t max_pairs = jade_max_pairs();
   // ≤ 8 threads pinned to neighbouring cores (one CCD on EPYC): the per-pair
   // barrier dominates otherwise (C5 on the MI355X host: 8 pinned threads 1.2 s,
   // 16 threads 2.4 s, unpinned 5–7 s). Affinities are restored afterwards.
@@ -790,11 +813,12 @@ Mat Solver::jade(size_t max_iter, double tol) {
       (void)pthread_setaffinity_np(pthread_self(), sizeof pin, &pin);
     }
     int buf = 0;
+    size_t done_pairs = 0;  // the same count on every thread
     for (size_t c = c0; c < c1; ++c) partial_g(pairs[0].first, pairs[0].second, c, &gpart[(0 * nch + c) * 3]);
 #pragma omp barrier
-    for (size_t it = 0; it < max_iter && !converged; ++it) {
+    for (size_t it = 0; it < max_iter && !converged && done_pairs < max_pairs; ++it) {
       double max_theta = 0.0;
-      for (size_t pi = 0; pi < pairs.size(); ++pi) {
+      for (size_t pi = 0; pi < pairs.size() && done_pairs < max_pairs; ++pi, ++done_pairs) {
         const size_t p = pairs[pi].first, q = pairs[pi].second;
         double g00 = 0, g01 = 0, g11 = 0;
         for (size_t c = 0; c < nch; ++c) {
@@ -841,10 +865,10 @@ Mat Solver::jade(size_t max_iter, double tol) {
       }
       if (tid == 0) {
         sweeps_done = it + 1;
-        if (cfg_.verbose && (it + 1) % 10 == 0)
+        if (verbose && (it + 1) % 10 == 0)
           std::printf("JADE iteration %zu: max angle = %s\n", it + 1, rust_e4(max_theta).c_str());
         if (max_theta < tol) {
-          if (cfg_.verbose) std::printf("JADE converged after %zu iterations\n", it + 1);
+          if (verbose) std::printf("JADE converged after %zu iterations\n", it + 1);
           converged = true;
         }
       }
@@ -852,12 +876,9 @@ Mat Solver::jade(size_t max_iter, double tol) {
     }
     if (pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof mine, &mine);
   }
-  (void)sweeps_done;
-  if (std::getenv("PICARD_TRACE")) {
-    const auto tj2 = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[picard-trace] jade: moments %.3f s, sweeps %.3f s\n",
-                 std::chrono::duration<double>(tj1 - tj0).count(), std::chrono::duration<double>(tj2 - tj1).count());
-  }
+  info->sweeps = sweeps_done;
+  info->converged = converged;
+  info->sweeps_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tj1).count();
   Mat w;
   if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
   return w;

@@ -12,6 +12,17 @@ namespace pcamd {
 
 std::string rust_e4(double v);  // Rust {:.4e}
 
+// jade.rs:22-72 on Y = base·(X − μ) (n × T, base n × nf): the fourth-moment
+// pass on the device, the cumulant matrices (jade.rs:78-131) and the Jacobi
+// sweeps, then sym_decorrelation(V) (jade.rs:69). Sweep placement:
+// AUTO = host; DEVICE = the cooperative device launch or an error; HOST; AUTO_DEVICE =
+// the device launch where supported, the host otherwise (PICARD_DEVICE_JADE=1).
+enum JadeSweeps { JADE_SWEEPS_AUTO = 0, JADE_SWEEPS_DEVICE = 1, JADE_SWEEPS_HOST = 2, JADE_SWEEPS_AUTO_DEVICE = 3 };
+struct JadeInfo { size_t sweeps = 0; bool converged = false; bool on_device = false; double moments_s = 0, sweeps_s = 0; };
+size_t jade_max_pairs();  // PICARD_JADE_MAX_PAIRS test hook (SIZE_MAX when unset)
+Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, double T, size_t max_iter,
+                    double tol, bool verbose, int where, JadeInfo* info);
+
 // src/lbfgs.rs:6-71 (only the parts core::run uses)
 struct LbfgsMemory {
   std::deque<Mat> s_list, y_list;

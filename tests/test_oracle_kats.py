@@ -100,3 +100,22 @@ def test_rust_e4_format(po):
     assert po.rust_e4(1.23456e-5) == "1.2346e-5"
     assert po.rust_e4(8.24883985) == "8.2488e0"
     assert po.rust_e4(-1234.5) == "-1.2345e3"
+
+
+def test_batched_jade_sweeps_match_literal_form(po, dg):
+    """oracle.jade_sweeps_batched (the matrix loop of jade.rs:137-167 vectorised, used
+    by the N = 64 GPU tests) against the literal per-matrix loop (po.jade) at C1 size,
+    and cumulants_from_moments against compute_cumulant_matrices (jade.rs:78-131)."""
+    x, _, _ = dg.generate_data(8, 10000, 42)
+    xc, _ = po.center(x)
+    x1, _ = po.whiten(xc, 8)
+    mats = np.stack(po.compute_cumulant_matrices(x1))
+    pairs = [(i, j) for i in range(8) for j in range(i, 8)]
+    z = np.stack([x1[i] * x1[j] for i, j in pairs])
+    assert np.max(np.abs(po.cumulants_from_moments(z @ z.T, 8, x1.shape[1]) - mats)) <= 1e-12
+    for it in (1, 3):
+        v, sweeps, _ = po.jade_sweeps_batched(mats, it)
+        assert sweeps == it
+        assert np.max(np.abs(po.sym_decorrelation(v) - po.jade(x1, it))) <= 1e-12
+    v, _, _ = po.jade_sweeps_batched(mats, 1, max_pairs=0)
+    assert np.array_equal(v, np.eye(8))

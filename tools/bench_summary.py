@@ -1,0 +1,18 @@
+"""Print the key numbers of a bench.py JSON line."""
+import json
+import sys
+
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print("value %.4g  ms/step %.1f  passes/iter %.2f  iters %s" % (d["value"], d["ms_per_step"], d["passes_per_iter"],
+                                                                d["iters_to_tol"]))
+if d.get("whole_fit"):
+    w = d["whole_fit"]
+    print("whole fit %.4g samples/s/iter  %.2f s  %.2f passes/iter" % (w["samples_per_s_per_iter"], w["iterations_s"],
+                                                                     w["passes_per_iter"]))
+for r in d.get("roofline_kernels", []):
+    print("  %-36s %8.2f ms  %.3f of peak  traffic %s" % (r["kernel"], r["avg_kernel_ms"], r["frac"], r["traffic"]))
+for k, c in (d.get("other_configs") or {}).items():
+    print("  %s %-48s iters %4d  setup %.2fs  iter %.2fs  %.3g samples/s/iter  passes %d  amari %.2e" % (
+        k, c["workload"], c["iters_to_tol"], c["setup_s"], c["iterations_s"], c["samples_per_s_per_iter"],
+        c["passes"], c["amari_vs_true_mixing"]))
+    print("      kernel ms", c["kernel_ms"], "launches", c["kernel_launches"])
