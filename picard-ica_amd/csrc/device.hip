@@ -2433,6 +2433,7 @@ struct DeviceCtx : Evaluator {
   double* d_tbuf = nullptr; size_t cap_tbuf = 0;   // y, ψ, ψ′ fragments of one T chunk
   double* d_slab = nullptr; size_t cap_slab = 0;
   double* d_trow = nullptr; size_t cap_trow = 0;
+  double tiled_budget_ = 0;  // bytes the fragment buffers may take (set on first use)
   static bool tiled_ok(size_t nc, int dens, double alpha) {
     return nc <= 256 && !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0)) && dens <= DENS_LINEAR;
   }
@@ -2514,8 +2515,16 @@ struct DeviceCtx : Evaluator {
     ensure(d_w, cap_w, wt.size());
     HIP_OK(hipMemcpyAsync(d_w, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
     const uint64_t n_tiles = (n_local_ + TL_TT - 1) / TL_TT;
-    // T chunks bound the fragment buffers to ~24 GB (3 arrays of ncp × chunk)
-    const uint64_t max_tiles = std::max<uint64_t>(1, (uint64_t)(24e9 / (3.0 * ncp * TL_TT * sizeof(double))));
+    // T chunks bound the fragment buffers (3 arrays of ncp × chunk) by what HBM
+    // has free next to X (at least 24 GB): C4 (256 × 1e7, 61 GB) is one chunk
+    if (tiled_budget_ == 0) {
+      size_t fr = 0, tot = 0;
+      HIP_OK(hipMemGetInfo(&fr, &tot));
+      const double have = (double)fr + (double)cap_tbuf * sizeof(double) - 16e9;
+      tiled_budget_ = std::max(24e9, std::min(have, 0.6 * (double)tot));
+    }
+    const uint64_t max_tiles =
+        std::max<uint64_t>(1, (uint64_t)(tiled_budget_ / (3.0 * ncp * TL_TT * sizeof(double))));
     const uint64_t ct = std::min<uint64_t>(n_tiles, max_tiles);
     const int nwg1 = ks ? (int)std::min<uint64_t>((uint64_t)n_cu * 2 / ((ncp / 16 + 7) / 8),
                                                   std::max<uint64_t>(ct * 4, 1))

@@ -1,5 +1,5 @@
 """Run BASELINE configs end-to-end on one GPU (device-generated bench mixture).
-Usage: python tools/run_configs.py C2 [C4 C5 ...] [--oracle]  → one JSON line per config."""
+Usage: python tools/run_configs.py C2 [C4 C5 ...] [--oracle] [--max-iter=K]  → one JSON line per config."""
 import json
 import os
 import sys
@@ -20,13 +20,14 @@ CONFIGS = {
 }
 
 
-def run(name, oracle=False):
+def run(name, oracle=False, max_iter=None):
     c = CONFIGS[name]
     n, t = c["n"], c["t"]
+    kw = dict(c["kw"], **({"max_iter": max_iter} if max_iter else {}))
     ctx = pa.DeviceContext(0)
     a = ctx.generate(n, t, 42)
     t0 = time.perf_counter()
-    s = pa.Solver(ctx, pa.PicardConfig(random_state=0, want_sources=False, **c["kw"]))
+    s = pa.Solver(ctx, pa.PicardConfig(random_state=0, want_sources=False, **kw))
     t_setup = time.perf_counter() - t0
     ctx.kernel_breakdown(reset=True)
     t1 = time.perf_counter()
@@ -55,5 +56,6 @@ def run(name, oracle=False):
 
 if __name__ == "__main__":
     want_oracle = "--oracle" in sys.argv
+    mi = [int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--max-iter=")]
     for name in [a for a in sys.argv[1:] if not a.startswith("--")]:
-        run(name, want_oracle)
+        run(name, want_oracle, mi[0] if mi else None)
