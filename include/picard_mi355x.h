@@ -25,6 +25,7 @@
  *                             G_raw = ÏˆÂ·Yáµ€ [, H_raw = Ïˆâ€²Â·(Yâˆ˜Y)áµ€], Î£Ïˆâ€², Î£â„“, Î£yÂ²
  *   pc_ctx_rowsum / pc_ctx_gram   centering and the whitening Gram XÂ·Xáµ€
  *   pc_ctx_sources            Y = WÂ·(Xâˆ’Î¼) materialised (PicardResult.sources)
+ *   pc_ctx_sources_device     the same Y kept in HBM (device pointer, one MFMA pass)
  *   pc_ctx_moments4 / pc_ctx_jade   the JADE warm start (src/jade.rs:22-197)
  *
  * Conventions: every matrix is row-major, contiguous, float64. Rows are
@@ -191,6 +192,14 @@ int pc_ctx_gram(pc_ctx* ctx, const double* mu /* or NULL */, double* out /* nf Ã
 /* this rank's shard of Y = WÂ·(Xâˆ’Î¼) â†’ host (nc Ã— n_local) */
 int pc_ctx_sources(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, double* out,
                    char* err, size_t errlen);
+/* The same Y kept in HBM for device-side consumers (solver.rs:182,199-214
+ * without the host round trip): the whole shard in one MFMA pass, nc rows of
+ * *ld_out doubles (row-major; columns past n_local are zero). *dev_out is a
+ * device pointer owned by the context, valid until the next
+ * pc_ctx_sources_device or pc_ctx_destroy; *kernel_ms = the pass's device time.
+ * Any out pointer may be NULL. */
+int pc_ctx_sources_device(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, const double** dev_out,
+                          uint64_t* ld_out, double* kernel_ms, char* err, size_t errlen);
 /* Î£_t z_p z_q over the pair products z_(i,j) = y_i y_j (i â‰¤ j) of Y = WÂ·(Xâˆ’Î¼):
  * the fourth-moment matrix JADE's cumulants are built from (src/jade.rs:91-113).
  * out: P Ã— P with P = nc(nc+1)/2, pairs in row-major (i â‰¤ j) order. */

@@ -168,6 +168,7 @@ def _load():
         "pc_ctx_gram": (C.c_int, [vp, d, d, cp, sz]),
         "pc_ctx_sources": (C.c_int, [vp, d, u64, d, d, cp, sz]),
         "pc_ctx_moments4": (C.c_int, [vp, d, u64, d, d, cp, sz]),
+        "pc_ctx_sources_device": (C.c_int, [vp, d, u64, d, P(C.c_void_p), P(u64), d, cp, sz]),
         "pc_ctx_jade": (C.c_int, [vp, d, u64, d, u64, C.c_double, i32, d, P(u64), cp, sz]),
         "pc_ctx_last_timing": (None, [vp, d, d]),
         "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
@@ -195,7 +196,7 @@ EXPORTED = [
     "pc_full_unmixing", "pc_mixing", "pc_result_free", "pc_amari_distance", "pc_permute",
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
-    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_moments4",
+    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
     "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
@@ -622,6 +623,17 @@ class DeviceContext:
         _raise(lib.pc_ctx_sources(self.h, _ptr(w), w.shape[0], _ptr(mu_a) if mu_a is not None else None,
                                   _ptr(out), err, len(err)), err)
         return out
+
+    def sources_device(self, w, mu=None):
+        """pc_ctx_sources_device: Y = w·(X − μ) kept in HBM. Returns (device pointer,
+        leading dimension in doubles, kernel ms); the buffer belongs to the context."""
+        w = _c64(w)
+        mu_a = _c64(mu) if mu is not None else None
+        p, ld, ms = C.c_void_p(), C.c_uint64(), C.c_double()
+        err = _errbuf()
+        _raise(lib.pc_ctx_sources_device(self.h, _ptr(w), w.shape[0], _ptr(mu_a) if mu_a is not None else None,
+                                         C.byref(p), C.byref(ld), C.byref(ms), err, len(err)), err)
+        return p.value, ld.value, ms.value
 
     def jade(self, w, mu=None, max_iter: int = 50, tol: float = 1e-6, where: str = "auto"):
         """pc_ctx_jade: the JADE warm start (jade.rs:22-72) on Y = w·(X − μ).

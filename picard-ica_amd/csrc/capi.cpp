@@ -17,6 +17,8 @@ Evaluator* make_device_ctx(int device, int rank, int world, const char* uid);
 void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0);
 void device_ctx_generate(Evaluator* e, uint64_t nf, uint64_t nt, uint64_t seed, double* a_out);
 void device_ctx_download(Evaluator* e, double* out);
+const double* device_ctx_sources_resident(Evaluator* e, const double* w, size_t nc, const double* mu, double* ms,
+                                          uint64_t* ld);
 uint64_t device_ctx_t0(const Evaluator* e);
 void device_ctx_timing(const Evaluator* e, double* k, double* c);
 void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double* mu, int dens, double alpha,
@@ -360,6 +362,18 @@ int pc_ctx_gram(pc_ctx* c, const double* mu, double* out, char* err, size_t errl
 int pc_ctx_sources(pc_ctx* c, const double* w, uint64_t nc, const double* mu, double* out, char* err,
                    size_t errlen) {
   return guarded(err, errlen, [&] { c->ev->sources(w, nc, mu, out); });
+}
+
+int pc_ctx_sources_device(pc_ctx* c, const double* w, uint64_t nc, const double* mu, const double** dev_out,
+                          uint64_t* ld_out, double* kernel_ms, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    uint64_t ld = 0;
+    double ms = 0.0;
+    const double* p = device_ctx_sources_resident(c->ev.get(), w, nc, mu, &ms, &ld);
+    if (dev_out) *dev_out = p;
+    if (ld_out) *ld_out = ld;
+    if (kernel_ms) *kernel_ms = ms;
+  });
 }
 
 int pc_ctx_moments4(pc_ctx* c, const double* w, uint64_t nc, const double* mu, double* out, char* err,

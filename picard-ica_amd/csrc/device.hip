@@ -35,7 +35,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef __attribute__((address_space(1))) void* gbl_vptr;
 
-enum { DENS_TANH = 0, DENS_EXP = 1, DENS_CUBE = 2, DENS_LINEAR = 3, DENS_NONE = 4 };
+// DENS_TANH_S / DENS_EXP_S: tanh / exp at any α (α ≤ 0 or NaN included — the
+// reference does not restrict it, density.rs:33-103), by the reference's own
+// formulas through libm instead of the α > 0 table paths; tiled path only.
+enum { DENS_TANH = 0, DENS_EXP = 1, DENS_CUBE = 2, DENS_LINEAR = 3, DENS_NONE = 4, DENS_TANH_S = 5, DENS_EXP_S = 6 };
 
 #define HIP_OK(expr)                                                                       \
   do {                                                                                     \
@@ -281,6 +284,30 @@ __device__ __forceinline__ void exp_n(const double* x, const double* tab, double
   }
 }
 
+// DENS_TANH_S / DENS_EXP_S per element (any α): ψ, ψ′ (density.rs:58-63, 96-103),
+// the raw Σψ′ term into dacc and the raw Σℓ term returned (density.rs:50-56,
+// 91-94), in the same mask-free row-term forms as the table paths (every term
+// vanishes at y = 0; finalize_row restores the per-sample constants).
+template <int DENS>
+__device__ __forceinline__ double safe_terms(double y, double alpha, double& dacc, double& psi, double& dpsi) {
+  if constexpr (DENS == DENS_TANH_S) {
+    const double th = tanh(alpha * y);
+    psi = th;
+    dacc = __builtin_fma(th, th, dacc);  // Σψ′ = α(n − Σ th²)
+    dpsi = alpha * (1.0 - th * th);
+    const double ay = fabs(y);
+    return ay + (log(1.0 + exp(-2.0 * alpha * ay)) - fm::LN2) / alpha;  // Σℓ = Σ(·) + n·ln2/α
+  } else {
+    const double y2 = y * y;
+    const double k = exp(-alpha / 2.0 * y2);
+    const double em = k - 1.0;
+    psi = y * k;
+    dpsi = (1.0 - alpha * y2) * k;
+    dacc += em - alpha * y2 * k;  // Σψ′ = n + Σ(k − 1 − αy²k)
+    return em;                    // Σℓ = −(n + Σ(k − 1))/α
+  }
+}
+
 // ψ (and ψ′ if NEED_D) of one 4-element fragment, NW elements interleaved at a
 // time (register budget); accumulates the row terms in element order, so the
 // sums do not depend on NW. Σy² only if NEED_Q (the reference uses Y∘Y only in
@@ -334,6 +361,14 @@ __device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m
         if constexpr (NEED_D) dpsi[g + i] = 3.0 * y2;
         a.l = __builtin_fma(y2, y2, a.l);
       }
+    } else if constexpr (DENS == DENS_TANH_S || DENS == DENS_EXP_S) {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        double p, d;
+        a.l += safe_terms<DENS>(y[g + i], alpha, a.d, p, d);
+        psi[g + i] = p;
+        if constexpr (NEED_D) dpsi[g + i] = d;
+      }
     } else {  // LINEAR: ψ = y turns G_raw into the Gram Σ y yᵀ; row terms unused
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
@@ -377,6 +412,12 @@ __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a,
         const double y2 = y[g + i] * y[g + i];
         a.l = __builtin_fma(y2, y2, a.l);
       }
+    } else if constexpr (DENS == DENS_TANH_S || DENS == DENS_EXP_S) {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        double d_unused = 0.0, p, d;
+        a.l += safe_terms<DENS>(y[g + i], alpha, d_unused, p, d);
+      }
     }
   }
 }
@@ -416,6 +457,8 @@ __device__ __forceinline__ double acc_dpsi(const RowAcc& a) {
 // raw row sum → statistic (c: 0 Σψ′, 1 Σℓ, 2 Σy²), n = valid samples of this shard
 __host__ __device__ inline double finalize_row(int dens, double alpha, double n, int c, double raw) {
   if (c == 2) return raw;
+  if (dens == DENS_TANH_S) dens = DENS_TANH;
+  if (dens == DENS_EXP_S) dens = DENS_EXP;
   if (dens == DENS_TANH) return c == 0 ? alpha * (n - raw) : raw + n * (0x1.62e42fefa39efp-1 / alpha);
   if (dens == DENS_EXP) return c == 0 ? n + raw : -(n + raw) / alpha;
   if (dens == DENS_CUBE) return c == 0 ? 3.0 * raw : 0.25 * raw;
@@ -1019,155 +1062,40 @@ __global__ void __launch_bounds__(256) k_reduce_rows(const double* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // Tiled two-phase pass for the shapes the register-resident fused kernel does
-// not cover: nc up to 256 (BASELINE C4: N = 256 non-ortho), nc ≤ 128 with H at
-// nc > 64, and any n_features (n_components < n_features).
-//   phase 1 (k_tiled_y): Y = W·(X−μ) per 128-sample tile as an LDS-tiled MFMA
-//     GEMM (W and X K-chunks of 32 staged in LDS), density, row sums, and
-//     y, ψ (, ψ′) written to HBM in MFMA-fragment order (512-B coalesced);
-//   phase 2 (k_tiled_gram): G_raw (, H_raw) = Σ_t ψ_t y_tᵀ (ψ′_t (y_t∘y_t)ᵀ) on
-//     MFMA, one 128×128 output tile per workgroup, T split over workgroups,
-//     fragments read straight from HBM into registers.
+// not cover: any n_components (BASELINE C4: N = 256 non-ortho), H at nc > 64,
+// any n_features (n_components < n_features), and tanh/exp at α ≤ 0.
+//   phase 1 (k_tiled_yw): Y = W·X̃ per 16-sample block on MFMA with W in VGPRs,
+//     density, row sums, and y, ψ (, ψ′) written to HBM in MFMA-fragment order
+//     (512-B coalesced); features beyond 256 come in chunks of 256 whose
+//     partial Y goes through the y buffer (MODE 2) and is picked up by the next
+//     chunk's chain (yin);
+//   phase 2 (k_tiled_gram2): G_raw (, H_raw) = Σ_t ψ_t y_tᵀ (ψ′_t (y_t∘y_t)ᵀ) on
+//     MFMA, one 128×128 output tile per workgroup, T split over workgroups.
 // ---------------------------------------------------------------------------
-constexpr int TL_TT = 64;   // samples per phase-1 tile
-constexpr int TL_KC = 32;   // K chunk staged in LDS
+constexpr int TL_TT = 64;   // samples per tile (fragment layout unit: 4 blocks of 16)
 constexpr int TL_TS = TL_TT / 16;
+constexpr int TL_KMAX = 256;  // features per phase-1 chunk (W fragments in VGPRs)
 
 __host__ __device__ inline size_t tl_frag(uint64_t tt, int ib, int ts, int r, int nib) {
   return ((((size_t)tt * nib + ib) * TL_TS + ts) * 4 + r) * 64;
 }
 
-template <int DENS, int MODE>  // MODE 0: full (write y, ψ, ψ′ + Σψ′, Σℓ, Σy²); 1: loss only (Σℓ, Σy²)
-__global__ void __launch_bounds__(FUSED_THREADS, 1)
-k_tiled_y(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int nfp, int ncp,
-          const double* __restrict__ WpT, const double* __restrict__ mu, double alpha, uint64_t tpw,
-          uint64_t n_tiles, double* __restrict__ partials, int accumulate, double* __restrict__ ybuf,
-          double* __restrict__ pbuf, double* __restrict__ dbuf) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int nib = ncp / 16;
-  const int npair = ncp / 32;             // i-block pairs; wave w owns pair w (if w < npair)
-  const bool active = wave < npair;
-  const double inv_alpha = 1.0 / alpha;
-  constexpr int WSTR = 256 + 16;          // ws row stride (doubles): k-major, rows contiguous, padded
-  constexpr int XSTR = TL_TT + 16;        // xs row stride
-  extern __shared__ double smem[];
-  double* ws = smem;                      // [TL_KC][WSTR]
-  double* xs = ws + TL_KC * WSTR;         // [TL_KC][XSTR]
-  double* rsb = xs + TL_KC * XSTR;        // [3][256] row sums of the workgroup
-  for (int e = tid; e < 3 * 256; e += FUSED_THREADS) rsb[e] = 0.0;
-  double rs_d[2] = {0, 0}, rs_l[2] = {0, 0}, rs_y[2] = {0, 0};
-  const uint64_t t_begin = (uint64_t)blockIdx.x * tpw;
-  const uint64_t t_end = t_begin + tpw < n_tiles ? t_begin + tpw : n_tiles;
-  for (uint64_t tt = t_begin; tt < t_end; ++tt) {
-    d4 acc[2][TL_TS];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int t = 0; t < TL_TS; ++t) acc[i][t] = d4{0, 0, 0, 0};
-    for (int k0 = 0; k0 < nfp; k0 += TL_KC) {
-      __syncthreads();  // previous chunk fully consumed
-      // W chunk: ws[k][row] = Wᵀ[k0 + k][row] (host stores W transposed: coalesced both sides)
-      for (int e = tid; e < ncp * TL_KC; e += FUSED_THREADS) {
-        const int k = e / ncp, row = e % ncp;
-        ws[k * WSTR + row] = WpT[(size_t)(k0 + k) * ncp + row];
-      }
-      // X chunk: xs[k][t] = X[k0 + k][tile + t] − μ (zero outside)
-      for (int e = tid; e < TL_KC * TL_TT / 2; e += FUSED_THREADS) {
-        const int k = e / (TL_TT / 2), t = 2 * (e % (TL_TT / 2));
-        const int kg = k0 + k;
-        const uint64_t tg = tt * TL_TT + t;
-        double2 v = double2{0.0, 0.0};
-        if (kg < nf) {
-          const double2 xv = *reinterpret_cast<const double2*>(X + (size_t)kg * ldx + tg);
-          const double m = mu ? mu[kg] : 0.0;
-          v.x = tg < n_local ? xv.x - m : 0.0;
-          v.y = tg + 1 < n_local ? xv.y - m : 0.0;
-        }
-        *reinterpret_cast<double2*>(xs + k * XSTR + t) = v;
-      }
-      __syncthreads();
-      if (active) {
-#pragma unroll
-        for (int kq = 0; kq < TL_KC / 4; ++kq) {
-          double a[TL_TS], b[2];
-#pragma unroll
-          for (int t = 0; t < TL_TS; ++t) a[t] = xs[(kq * 4 + lk) * XSTR + t * 16 + lr];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) b[i] = ws[(kq * 4 + lk) * WSTR + (wave * 2 + i) * 16 + lr];
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int t = 0; t < TL_TS; ++t) acc[i][t] = mfma(a[t], b[i], acc[i][t]);
-        }
-      }
-    }
-    if (active) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int ib = wave * 2 + i;
-#pragma unroll
-        for (int t = 0; t < TL_TS; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const double y = acc[i][t][r];
-            const bool valid = tt * TL_TT + t * 16 + 4 * r + lk < n_local;
-            const size_t f = tl_frag(tt, ib, t, r, nib) + lane;
-            if constexpr (MODE == 0) {
-              double psi, dpsi, ll;
-              density_eval<DENS, true>(y, alpha, inv_alpha, psi, dpsi, ll);
-              rs_d[i] += valid ? dpsi : 0.0;
-              rs_l[i] += valid ? ll : 0.0;
-              ybuf[f] = y;
-              pbuf[f] = psi;
-              if (dbuf) dbuf[f] = valid ? dpsi : 0.0;
-            } else {
-              rs_l[i] += valid ? density_loss<DENS>(y, alpha, inv_alpha) : 0.0;
-            }
-            rs_y[i] = __builtin_fma(y, y, rs_y[i]);
-          }
-      }
-    }
-  }
-  // row sums → workgroup partials [Σψ′ | Σℓ | Σy²] (ncp each)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    rs_d[i] += __shfl_xor(rs_d[i], 16); rs_d[i] += __shfl_xor(rs_d[i], 32);
-    rs_l[i] += __shfl_xor(rs_l[i], 16); rs_l[i] += __shfl_xor(rs_l[i], 32);
-    rs_y[i] += __shfl_xor(rs_y[i], 16); rs_y[i] += __shfl_xor(rs_y[i], 32);
-  }
-  __syncthreads();
-  if (active && lk == 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (wave * 2 + i) * 16 + lr;
-      rsb[row] = rs_d[i];
-      rsb[256 + row] = rs_l[i];
-      rsb[512 + row] = rs_y[i];
-    }
-  }
-  __syncthreads();
-  double* out = partials + (size_t)blockIdx.x * 3 * ncp;
-  for (int e = tid; e < 3 * ncp; e += FUSED_THREADS) {
-    const double v = rsb[(e / ncp) * 256 + e % ncp];
-    out[e] = accumulate ? out[e] + v : v;
-  }
-}
-
-// Phase 1 with W in registers (nf ≤ 256): the workgroup pair-member
-// blockIdx.y = role owns output rows [128·role, 128·role + 128); wave w owns
-// row block ib = 8·role + w and keeps its W fragment (16 rows × NFP) in VGPRs
-// for the whole launch, so W is read once — the LDS-chunked k_tiled_y re-read
-// all of W from L2 for every 64-sample tile (4× the X traffic at N = 256).
-// X̃ blocks of 16 samples × NFP features are staged through LDS (shared by the
-// 8 waves; double-buffered, prefetch pinned one block ahead) and Yᵀ tiles come
-// from ONE chain of KS MFMAs per wave, as in k_eval_fused. Row terms use the
-// mask-free RowAcc (raw sums, finalized in k_reduce_tiled).
-template <int KS, int DENS, int MODE>  // MODE 0: y, ψ (, ψ′) fragments + all row terms; 1: Σℓ, Σy² terms only
+// Phase 1 with W in registers: the workgroup role blockIdx.y owns output rows
+// [128·role, 128·role + 128); wave w owns row block ib = 8·role + w and keeps
+// its W fragment (16 rows × 4·KS features of this chunk) in VGPRs for the whole
+// launch, so W is read once. X̃ blocks of 16 samples × 4·KS features are staged
+// by LDS-DMA (shared by the 8 waves; double-buffered, one barrier per block)
+// and Yᵀ tiles come from ONE chain of KS MFMAs per wave, as in k_eval_fused.
+// Row terms use the mask-free RowAcc (raw sums, finalized in k_reduce_tiled).
+// MODE 0: y, ψ (, ψ′) fragments + all row terms; 1: Σℓ, Σy² terms only;
+// 2: partial y of a feature chunk only. yin (MODE 0/1/2, may alias ybuf): the
+// partial y of the earlier feature chunks, added at the start of each chain.
+template <int KS, int DENS, int MODE>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, int ncp,
            const double* __restrict__ WpT, const double* __restrict__ mu, double alpha, uint64_t bpw,
-           uint64_t n_blocks, double* __restrict__ partials, int accumulate, double* __restrict__ ybuf,
-           double* __restrict__ pbuf, double* __restrict__ dbuf) {
+           uint64_t n_blocks, double* __restrict__ partials, int accumulate, double* ybuf,
+           double* __restrict__ pbuf, double* __restrict__ dbuf, const double* yin) {
   constexpr int NFP = 4 * KS, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave per block
   static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1187,11 +1115,11 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   RowAcc racc;
   const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
-  const uint64_t b_last = b_end - 1;
   // X staged by LDS-DMA (the centred resident X: μ = null; samples past n_in are
   // the zero padding of X, rows ≥ nf read row 0 against zero W columns): wave w
   // moves rows [w·NFP/8, (w+1)·NFP/8), 8 rows × 16 samples per instruction
   (void)mu;
+  (void)n_in;
   const double* src[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
@@ -1211,33 +1139,41 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
     for (uint64_t b = b_begin; b < b_end; ++b) {
       if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
       if (active) {
+        const uint64_t tt = b >> 2;
+        const int ts = (int)(b & 3);
+        const size_t f0 = tl_frag(tt, ib, ts, 0, nib) + lane;
         d4 yv = d4{0, 0, 0, 0};
+        if (yin)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yv[r] = yin[f0 + 64 * r];
         const double* xrow = xs0 + cur * XS + lk * 16 + lr;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
         if constexpr (MODE == 0) {
           double psi[4], dpsi[4];
           density_acc4<DENS, true, true, 1>(yv, alpha_, m2a, s_exp_tab, racc, psi, dpsi);
-          const uint64_t tt = b >> 2;
-          const int ts = (int)(b & 3);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const size_t f = tl_frag(tt, ib, ts, r, nib) + lane;
-            ybuf[f] = yv[r];
-            pbuf[f] = psi[r];
-            if (dbuf) dbuf[f] = dpsi[r];
+            ybuf[f0 + 64 * r] = yv[r];
+            pbuf[f0 + 64 * r] = psi[r];
+            if (dbuf) dbuf[f0 + 64 * r] = dpsi[r];
           }
-        } else {
+        } else if constexpr (MODE == 1) {
           loss_acc4<DENS, true, 1>(yv, alpha_, m2a, s_exp_tab, racc);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ybuf[f0 + 64 * r] = yv[r];
         }
-        if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc);
+        if constexpr (MODE != 2)
+          if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc);
       }
       __syncthreads();  // also waits for this wave's LDS-DMA of block b + 1
       cur ^= 1;
     }
   }
-  // raw row terms → workgroup partials [Σψ′ | Σℓ | Σy²] (ncp each); the two
-  // roles of a slot write disjoint rows
+  if constexpr (MODE == 2) return;
+  // raw row terms → workgroup partials [Σψ′ | Σℓ | Σy²] (ncp each); the roles
+  // of a slot write disjoint rows
   const int nfac = b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0;  // one density call per block
   double rs_d = acc_dpsi<DENS>(racc), rs_l = acc_ll<DENS>(racc, inv_alpha, nfac), rs_q = racc.q;
   rs_d += __shfl_xor(rs_d, 16); rs_d += __shfl_xor(rs_d, 32);
@@ -1657,112 +1593,71 @@ __global__ void __launch_bounds__(256) k_reduce(const double* __restrict__ parti
 }
 
 // ---------------------------------------------------------------------------
-// Generic path (shapes the fused kernel does not cover: nc > 128, nf > 128,
-// or few rows with many features). Y is materialised per T-chunk.
+// Y = W·X̃ materialised row-major (solver.rs:182,199-214 sources / transform;
+// benchmarks.rs:34 X = A·S; the Y chunks of the JADE moments). W fragments live
+// in VGPRs for the whole launch (read once), X̃ blocks of 16 samples × 4·KS
+// features are staged by LDS-DMA (double-buffered, one barrier per block) and
+// each wave runs ONE chain of KS MFMAs per 16×16 tile with W as the A operand,
+// so by the f64 C/D map lane l holds Y[16·ib + (l>>4) + 4r][16·b + (l&15)]:
+// every store instruction writes 4 rows × 128 contiguous bytes. blockIdx.y
+// picks 8 row blocks (128 rows); feature counts above 4·KS come in chunks of
+// 4·KS (host loop; `accumulate` adds the partial product already in Y).
+// Samples ≥ n_out are computed from X's zero padding and never stored.
 // ---------------------------------------------------------------------------
-// Y = W·(X − μ) (+ ψ, ψ′, ℓ) for chunk columns [c0, c0+cn). One thread per sample.
-template <int DENS>
-__global__ void k_ycomp(const double* __restrict__ X, uint64_t ldx, uint64_t n_valid, int nf, int nc,
-                        const double* __restrict__ W, const double* __restrict__ mu, double alpha,
-                        uint64_t c0, uint64_t cn, double* __restrict__ Y, uint64_t ldy,
-                        double* __restrict__ P, double* __restrict__ D, double* __restrict__ L,
-                        uint64_t ldc) {
-  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (t >= cn) return;
-  const uint64_t tg = c0 + t;
-  const bool valid = tg < n_valid;
-  constexpr int RB = 8;
-  for (int i0 = 0; i0 < nc; i0 += RB) {
-    double acc[RB];
+template <int KS>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_ystore(const double* __restrict__ X, uint64_t ldx, int nrows_x, const double* __restrict__ WpT, int ncp, int nc,
+         uint64_t n_out, uint64_t bpw, uint64_t n_blocks, double* __restrict__ Y, uint64_t ldy, int accumulate) {
+  constexpr int NFP = 4 * KS, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave per block
+  static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int ib = blockIdx.y * 8 + wave;
+  const bool active = ib < ncp / 16;
+  extern __shared__ double smem[];
+  double* xs0 = smem;  // [2][NFP][16]
+  double wf[KS];
 #pragma unroll
-    for (int r = 0; r < RB; ++r) acc[r] = 0.0;
-    for (int k = 0; k < nf; ++k) {
-      const double xv = valid ? X[(size_t)k * ldx + tg] - (mu ? mu[k] : 0.0) : 0.0;
+  for (int ks = 0; ks < KS; ++ks) wf[ks] = active ? WpT[(size_t)(4 * ks + lk) * ncp + ib * 16 + lr] : 0.0;
+  const double* src[NU];
 #pragma unroll
-      for (int r = 0; r < RB; ++r)
-        if (i0 + r < nc) acc[r] = fma(W[(size_t)(i0 + r) * nf + k], xv, acc[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      if (i0 + r >= nc) break;
-      const double y = acc[r];
-      if (Y) Y[(size_t)(i0 + r) * ldy + t] = y;
-      if constexpr (DENS != DENS_NONE) {
-        double psi, dpsi, ll;
-        density_eval<DENS, false>(y, alpha, 1.0 / alpha, psi, dpsi, ll);
-        P[(size_t)(i0 + r) * ldc + t] = psi;
-        D[(size_t)(i0 + r) * ldc + t] = valid ? dpsi : 0.0;
-        L[(size_t)(i0 + r) * ldc + t] = valid ? ll : 0.0;
-      }
-    }
+  for (int u = 0; u < NU; ++u) {
+    const int xr = wave * (NFP / 8) + 8 * u + (lane >> 3);
+    src[u] = X + (size_t)(xr < nrows_x ? xr : 0) * ldx + 2 * (lane & 7);  // rows ≥ nrows_x: zero W columns
   }
-}
-
-// out[s][i][j] += Σ_{t in split s} A[i][t]·B[j][t]  (B squared when SQ)
-// 16×16 threads, each a 4×4 output micro-tile of a 64×64 tile; K staged 32 wide.
-template <bool SQ>
-__global__ void __launch_bounds__(256) k_gemm_nt(const double* __restrict__ A, const double* __restrict__ B,
-                                                 uint64_t ld, int m, uint64_t kn, int splits,
-                                                 double* __restrict__ out) {
-  __shared__ double as[64][33];
-  __shared__ double bs[64][33];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int tiles = (m + 63) / 64;
-  const int tile = blockIdx.x % (tiles * tiles), s = blockIdx.x / (tiles * tiles);
-  const int ti = tile / tiles, tj = tile % tiles;
-  const uint64_t per = (kn + splits - 1) / splits;
-  const uint64_t k0 = (uint64_t)s * per, k1 = std::min<uint64_t>(kn, k0 + per);
-  double acc[4][4] = {};
-  for (uint64_t kb = k0; kb < k1; kb += 32) {
-    for (int e = threadIdx.x; e < 64 * 32; e += 256) {
-      const int r = e / 32, c = e % 32;
-      const int gi = ti * 64 + r, gj = tj * 64 + r;
-      const uint64_t kk = kb + c;
-      as[r][c] = (gi < m && kk < k1) ? A[(size_t)gi * ld + kk] : 0.0;
-      double bv = (gj < m && kk < k1) ? B[(size_t)gj * ld + kk] : 0.0;
-      bs[r][c] = SQ ? bv * bv : bv;
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int c = 0; c < 32; ++c) {
-      double av[4], bv[4];
+  auto stage = [&](uint64_t b, double* xs) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { av[u] = as[ty * 4 + u][c]; bv[u] = bs[tx * 4 + u][c]; }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] = fma(av[u], bv[v], acc[u][v]);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int gi = ti * 64 + ty * 4 + u, gj = tj * 64 + tx * 4 + v;
-      if (gi < m && gj < m) out[((size_t)s * m + gi) * m + gj] += acc[u][v];
-    }
-}
-
-// per-row sums over the chunk: acc[which][row] += Σ_t src_which[row][t]
-__global__ void k_rowsums_chunk(const double* __restrict__ D, const double* __restrict__ L,
-                                const double* __restrict__ Y, uint64_t ldc, uint64_t ldy, uint64_t cn,
-                                uint64_t n_valid_in_chunk, double* __restrict__ acc, int nc) {
-  const int row = blockIdx.x, which = blockIdx.y;
-  __shared__ double red[256];
-  double s = 0.0;
-  for (uint64_t t = threadIdx.x; t < cn; t += blockDim.x) {
-    if (which == 0) s += D[(size_t)row * ldc + t];
-    else if (which == 1) s += L[(size_t)row * ldc + t];
-    else { const double y = t < n_valid_in_chunk ? Y[(size_t)row * ldy + t] : 0.0; s += y * y; }
-  }
-  red[threadIdx.x] = s;
+    for (int u = 0; u < NU; ++u)
+      __builtin_amdgcn_global_load_lds((gbl_vptr)(src[u] + b * 16),
+                                       (lds_vptr)(xs + (wave * (NFP / 8) + 8 * u) * 16), 16, 0, 0);
+  };
+  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  if (b_begin >= b_end) return;
+  stage(b_begin, xs0);
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
+  int cur = 0;
+  for (uint64_t b = b_begin; b < b_end; ++b) {
+    if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
+    if (active) {
+      d4 yv = d4{0, 0, 0, 0};
+      const double* xrow = xs0 + cur * XS + lk * 16 + lr;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) yv = mfma(wf[ks], xrow[(4 * ks) * 16], yv);
+      const uint64_t t = b * 16 + lr;
+      if (t < n_out)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = ib * 16 + lk + 4 * r;
+          if (row < nc) {
+            double* p = Y + (size_t)row * ldy + t;
+            *p = accumulate ? *p + yv[r] : yv[r];
+          }
+        }
+    }
+    __syncthreads();  // also waits for this wave's LDS-DMA of block b + 1
+    cur ^= 1;
   }
-  if (threadIdx.x == 0) acc[which * nc + row] += red[0];
 }
 
 __global__ void k_sum_slabs(const double* __restrict__ slabs, int splits, size_t n, double* __restrict__ out) {
@@ -2029,7 +1924,7 @@ struct DeviceCtx : Evaluator {
   ~DeviceCtx() override {
     (void)hipSetDevice(device);
     if (comm) ncclCommDestroy(comm);
-    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part})
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src})
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -2099,25 +1994,70 @@ struct DeviceCtx : Evaluator {
       A[e] = (double)(st >> 33) / 2147483648.0 - 0.5;
     }
     if (a_out) std::memcpy(a_out, A.data(), A.size() * sizeof(double));
-    double* dA = ensure(d_w, cap_w, nf * nf);
-    HIP_OK(hipMemcpyAsync(dA, A.data(), A.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    ystore_upload(A.data(), nf, nf);
     const Affine jt = lcg_jump(n_tot);  // row i → i+1 at fixed t
-    const uint64_t CH = 1ull << 20;
+    const uint64_t CH = 1ull << 22;
     double* S = ensure(d_chunk, cap_chunk, nf * CH);
     for (uint64_t c0 = 0; c0 < nl; c0 += CH) {
       const uint64_t cn = std::min<uint64_t>(CH, nl - c0);
       k_gen_sources<<<(cn + 255) / 256, 256, 0, stream>>>(S, CH, (int)nf, tt0 + c0, cn, seed, jt.a, jt.c);
       HIP_OK(hipGetLastError());
-      // X[:, c0:c0+cn] = A·S (benchmarks.rs:34)
-      k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(S, CH, cn, (int)nf, (int)nf, dA, nullptr, 0.0, 0, cn,
-                                                               X + c0, ldx, nullptr, nullptr, nullptr, 0);
-      HIP_OK(hipGetLastError());
+      // X[:, c0:c0+cn] = A·S (benchmarks.rs:34) on MFMA; the padding past n_local stays zero
+      ystore_run(S, CH, nf, nf, cn, X + c0, ldx);
     }
     HIP_OK(hipStreamSynchronize(stream));
   }
 
   void allreduce(double* d, size_t n) {
     if (comm) RCCL_OK(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm, stream));
+  }
+
+  // ---- Y = W·Xs stored row-major on MFMA (k_ystore) ------------------------
+  // w: host nc × nrows row-major; Xs: device, nrows × (≥ 16·⌈n_out/16⌉) with
+  // leading dimension lds and 16-B aligned rows; Y: device nc × n_out, ld ldy.
+  double* d_wys = nullptr; size_t cap_wys = 0;
+  static int ystore_ks(uint64_t nrows) { return nrows <= 64 ? 16 : nrows <= 128 ? 32 : 64; }
+  template <int KS>
+  void ystore_ks_launch(const double* Xs, uint64_t lds, uint64_t nrows, const double* dwt, int ncp, size_t nc,
+                        uint64_t n_out, double* Y, uint64_t ldy) {
+    static bool attr = false;
+    if (!attr) {
+      HIP_OK(hipFuncSetAttribute((const void*)k_ystore<KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 2 * 16 * 4 * KS * (int)sizeof(double)));
+      attr = true;
+    }
+    const uint64_t n_blocks = (n_out + 15) / 16;
+    const int nroles = (ncp / 16 + 7) / 8;
+    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(n_blocks, (uint64_t)2 * n_cu / nroles + 1));
+    const uint64_t bpw = (n_blocks + want - 1) / want;
+    const unsigned nwg = (unsigned)((n_blocks + bpw - 1) / bpw);
+    constexpr int CHK = 4 * KS;
+    for (uint64_t k0 = 0; k0 < nrows; k0 += CHK)
+      k_ystore<KS><<<dim3(nwg, nroles), FUSED_THREADS, (size_t)2 * 16 * CHK * sizeof(double), stream>>>(
+          Xs + k0 * lds, lds, (int)std::min<uint64_t>(CHK, nrows - k0), dwt + k0 * ncp, ncp, (int)nc, n_out, bpw,
+          n_blocks, Y, ldy, k0 > 0 ? 1 : 0);
+    HIP_OK(hipGetLastError());
+  }
+  // Wᵀ (zero-padded to whole chunks and row blocks) into d_wys, once per map
+  void ystore_upload(const double* w, size_t nc, uint64_t nrows) {
+    const uint64_t chk = 4 * (uint64_t)ystore_ks(nrows), nfp = (nrows + chk - 1) / chk * chk;
+    const size_t ncp = (nc + 15) / 16 * 16;
+    std::vector<double> wt((size_t)nfp * ncp, 0.0);
+    for (size_t i = 0; i < nc; ++i)
+      for (size_t k = 0; k < nrows; ++k) wt[k * ncp + i] = w[i * nrows + k];
+    ensure(d_wys, cap_wys, wt.size());
+    HIP_OK(hipMemcpyAsync(d_wys, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));  // the host image must outlive the copy; the kernels stay async
+  }
+  // Y[:, :n_out] = W·Xs with the map of the last ystore_upload (same nc, nrows)
+  void ystore_run(const double* Xs, uint64_t lds, uint64_t nrows, size_t nc, uint64_t n_out, double* Y, uint64_t ldy) {
+    if (n_out == 0 || nc == 0) return;
+    const int ncp = (int)((nc + 15) / 16 * 16);
+    switch (ystore_ks(nrows)) {
+      case 16: ystore_ks_launch<16>(Xs, lds, nrows, d_wys, ncp, nc, n_out, Y, ldy); break;
+      case 32: ystore_ks_launch<32>(Xs, lds, nrows, d_wys, ncp, nc, n_out, Y, ldy); break;
+      default: ystore_ks_launch<64>(Xs, lds, nrows, d_wys, ncp, nc, n_out, Y, ldy); break;
+    }
   }
 
   // this shard's row sums of the resident X into st (device), no all-reduce;
@@ -2302,7 +2242,7 @@ struct DeviceCtx : Evaluator {
         default: dispatch_h<8>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
       }
     } else {
-      generic_eval(w, nc, dmu, dens, alpha, need_h, st);
+      throw computation_error("no evaluation path for density id " + std::to_string(dens));
     }
     allreduce(st, total);
     HIP_OK(hipMemcpyAsync(stats_host, st, total * sizeof(double), hipMemcpyDeviceToHost, stream));
@@ -2435,81 +2375,81 @@ struct DeviceCtx : Evaluator {
   double* d_trow = nullptr; size_t cap_trow = 0;
   double tiled_budget_ = 0;  // bytes the fragment buffers may take (set on first use)
   static bool tiled_ok(size_t nc, int dens, double alpha) {
-    return nc <= 256 && !((dens == DENS_TANH || dens == DENS_EXP) && !(alpha > 0.0)) && dens <= DENS_LINEAR;
+    (void)nc;
+    (void)alpha;
+    return dens <= DENS_LINEAR;  // any shape; tanh/exp at α ≤ 0 through the libm forms
   }
-  // register-W phase 1 (k_tiled_yw) for nf ≤ 256: K steps per MFMA chain, 0 = use k_tiled_y
-  static int yw_ks(uint64_t nf) { return nf <= 64 ? 16 : nf <= 128 ? 32 : nf <= 256 ? 64 : 0; }
+  // the density id the tiled kernels run: the libm forms for tanh/exp unless α > 0
+  static int tiled_dens(int dens, double alpha) {
+    if (dens == DENS_TANH && !(alpha > 0.0)) return DENS_TANH_S;
+    if (dens == DENS_EXP && !(alpha > 0.0)) return DENS_EXP_S;
+    return dens;
+  }
+  // K steps per MFMA chain of phase 1 (one chunk of ≤ 256 features)
+  static int yw_ks(uint64_t nf) { return nf <= 64 ? 16 : nf <= 128 ? 32 : 64; }
   template <int KS, int D>
-  void yw_launch_ks(int mode, int ncp, const double* dmu, double alpha, uint64_t ntl, int nwg1, bool acc,
-                    const double* X0, uint64_t n_in, double* yb, double* pb, double* db) {
+  void yw_launch_ks(int mode, int ncp, double alpha, uint64_t ntl, int nwg1, bool acc, const double* X0,
+                    uint64_t nrows, const double* wpt, double* yb, double* pb, double* db, const double* yin) {
     const uint64_t n_blocks = ntl * 4;  // whole 64-sample tiles: phase 2 reads every sub-block
     const uint64_t bpw = (n_blocks + nwg1 - 1) / nwg1;
     const int nroles = (ncp / 16 + 7) / 8;
     const size_t lds = (size_t)2 * 16 * 4 * KS * sizeof(double);
-    auto k = mode == 0 ? k_tiled_yw<KS, D, 0> : k_tiled_yw<KS, D, 1>;
-    static bool attr[2] = {false, false};
+    auto k = mode == 0 ? k_tiled_yw<KS, D, 0> : mode == 1 ? k_tiled_yw<KS, D, 1> : k_tiled_yw<KS, D, 2>;
+    static bool attr[3] = {false, false, false};
     if (!attr[mode]) {
       HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
       attr[mode] = true;
     }
-    k<<<dim3(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, n_in, (int)nf, ncp, d_w, dmu, alpha, bpw,
-                                                          n_blocks, d_trow, acc ? 1 : 0, yb, pb, db);
+    k<<<dim3(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, 0, (int)nrows, ncp, wpt, nullptr, alpha, bpw,
+                                                          n_blocks, d_trow, acc ? 1 : 0, yb, pb, db, yin);
   }
   template <int D>
-  void yw_launch(int mode, int ncp, const double* dmu, double alpha, uint64_t ntl, int nwg1, bool acc,
-                 const double* X0, uint64_t n_in, double* yb, double* pb, double* db) {
-    switch (yw_ks(nf)) {
-      case 16: yw_launch_ks<16, D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in, yb, pb, db); break;
-      case 32: yw_launch_ks<32, D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in, yb, pb, db); break;
-      default: yw_launch_ks<64, D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in, yb, pb, db); break;
+  void yw_launch(int ks, int mode, int ncp, double alpha, uint64_t ntl, int nwg1, bool acc, const double* X0,
+                 uint64_t nrows, const double* wpt, double* yb, double* pb, double* db, const double* yin) {
+    switch (ks) {
+      case 16: yw_launch_ks<16, D>(mode, ncp, alpha, ntl, nwg1, acc, X0, nrows, wpt, yb, pb, db, yin); break;
+      case 32: yw_launch_ks<32, D>(mode, ncp, alpha, ntl, nwg1, acc, X0, nrows, wpt, yb, pb, db, yin); break;
+      default: yw_launch_ks<64, D>(mode, ncp, alpha, ntl, nwg1, acc, X0, nrows, wpt, yb, pb, db, yin); break;
     }
   }
+  // one T chunk: phase 1 over the feature chunks (partial y through the y
+  // buffer), then phase 2 (mode 0)
   template <int D>
-  void tiled_launch(int mode, int nfp, int ncp, const double* dmu, double alpha, uint64_t tile0, uint64_t ntl,
-                    bool need_h, int nsplit, int nwg1, uint64_t tpw, bool acc, const double* X0) {
-    (void)tile0;
+  void tiled_launch(int mode, int ks, int ncp, double alpha, uint64_t ntl, bool need_h, int nsplit, int nwg1, bool acc,
+                    const double* X0) {
     const size_t chunk = (size_t)ncp * ntl * TL_TT;
     double* yb = d_tbuf;
     double* pb = d_tbuf + chunk;
     double* db = need_h ? d_tbuf + 2 * chunk : nullptr;
-    const size_t lds = (size_t)(TL_KC * (256 + 16) + TL_KC * (TL_TT + 16) + 3 * 256) * sizeof(double);
-    static bool attr[2] = {false, false};
-    auto k1 = mode == 0 ? k_tiled_y<D, 0> : k_tiled_y<D, 1>;
-    if (!attr[mode]) {
-      HIP_OK(hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr[mode] = true;
+    const uint64_t kc = 4 * (uint64_t)ks;  // features per chunk
+    for (uint64_t k0 = 0; k0 < nf; k0 += kc) {
+      const bool last = k0 + kc >= nf;
+      yw_launch<D>(ks, last ? mode : 2, ncp, alpha, ntl, nwg1, acc, X0 + k0 * ldx, std::min<uint64_t>(kc, nf - k0),
+                   d_w + k0 * ncp, yb, pb, db, k0 > 0 ? yb : nullptr);
+      HIP_OK(hipGetLastError());
     }
-    const uint64_t n_in_chunk = std::min<uint64_t>(n_local_ - tile0 * TL_TT, ntl * TL_TT);
-    if (yw_ks(nf)) {
-      yw_launch<D>(mode, ncp, dmu, alpha, ntl, nwg1, acc, X0, n_in_chunk, yb, pb, db);
-    } else {
-      k1<<<nwg1, FUSED_THREADS, lds, stream>>>(X0, ldx, n_in_chunk, (int)nf, nfp, ncp, d_w, dmu, alpha, tpw, ntl,
-                                               d_trow, acc ? 1 : 0, yb, pb, db);
-    }
-    HIP_OK(hipGetLastError());
     if (mode == 0) {
       const int nto = (ncp / 16 + 7) / 8;
       const uint64_t tps = (ntl + nsplit - 1) / nsplit;
-      {
-        const size_t lds2 = (size_t)2 * (need_h ? 3 : 2) * 8 * 256 * sizeof(double);
-        static bool attr2[2] = {false, false};
-        auto k2 = need_h ? k_tiled_gram2<true> : k_tiled_gram2<false>;
-        if (!attr2[need_h]) {
-          HIP_OK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-          attr2[need_h] = true;
-        }
-        k2<<<dim3(nto * nto, nsplit), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      const size_t lds2 = (size_t)2 * (need_h ? 3 : 2) * 8 * 256 * sizeof(double);
+      static bool attr2[2] = {false, false};
+      auto k2 = need_h ? k_tiled_gram2<true> : k_tiled_gram2<false>;
+      if (!attr2[need_h]) {
+        HIP_OK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr2[need_h] = true;
       }
+      k2<<<dim3(nto * nto, nsplit), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
       HIP_OK(hipGetLastError());
     }
   }
   // mode 0: all stats; mode 1: Σℓ, Σy² only (loss-only try; the completion recomputes)
   void tiled_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st,
                   int mode) {
+    if (dmu) throw computation_error("tiled pass expects the centred resident X");
     const int ncp = (int)((nc + 31) / 32 * 32);
     const int ks = yw_ks(nf);
-    const int nfp = ks ? 4 * ks : (int)((nf + TL_KC - 1) / TL_KC * TL_KC);  // k_tiled_yw reads 4·KS rows
-    std::vector<double> wt((size_t)nfp * ncp, 0.0);  // Wᵀ, zero-padded
+    const uint64_t kc = 4 * (uint64_t)ks, nfp = (nf + kc - 1) / kc * kc;
+    std::vector<double> wt((size_t)nfp * ncp, 0.0);  // Wᵀ, zero-padded to whole feature chunks
     for (size_t i = 0; i < nc; ++i)
       for (size_t k = 0; k < nf; ++k) wt[k * ncp + i] = w[i * nf + k];
     ensure(d_w, cap_w, wt.size());
@@ -2525,70 +2465,33 @@ struct DeviceCtx : Evaluator {
     }
     const uint64_t max_tiles =
         std::max<uint64_t>(1, (uint64_t)(tiled_budget_ / (3.0 * ncp * TL_TT * sizeof(double))));
-    const uint64_t ct = std::min<uint64_t>(n_tiles, max_tiles);
-    const int nwg1 = ks ? (int)std::min<uint64_t>((uint64_t)n_cu * 2 / ((ncp / 16 + 7) / 8),
-                                                  std::max<uint64_t>(ct * 4, 1))
-                        : (int)std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>(ct, 1));
+    const uint64_t ct = std::min<uint64_t>(std::max<uint64_t>(n_tiles, 1), max_tiles);
+    const int nroles = (ncp / 16 + 7) / 8;
+    const int nwg1 = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_cu * 2 / nroles, ct * 4));
     const int nto = (ncp / 16 + 7) / 8;
     const int nsplit = (int)std::max<uint64_t>(1, std::min<uint64_t>(ct, (uint64_t)(2 * n_cu / (nto * nto))));
-    if (mode == 0) {
-      ensure(d_tbuf, cap_tbuf, (size_t)(need_h ? 3 : 2) * ncp * ct * TL_TT);
-      ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
-    }
+    // y buffer: always in mode 0; in mode 1 only to carry partial y across feature chunks
+    if (mode == 0) ensure(d_tbuf, cap_tbuf, (size_t)(need_h ? 3 : 2) * ncp * ct * TL_TT);
+    else if (nf > kc) ensure(d_tbuf, cap_tbuf, (size_t)ncp * ct * TL_TT);
+    if (mode == 0) ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
     ensure(d_trow, cap_trow, (size_t)nwg1 * 3 * ncp);
+    const int td = tiled_dens(dens, alpha);
     for (uint64_t t0 = 0; t0 < std::max<uint64_t>(n_tiles, 1); t0 += ct) {
-      const uint64_t ntl = std::min<uint64_t>(ct, n_tiles - t0);
-      const uint64_t tpw = (ntl + nwg1 - 1) / nwg1;
+      const uint64_t ntl = std::min<uint64_t>(ct, std::max<uint64_t>(n_tiles, 1) - t0);
       const bool acc = t0 > 0;
       const double* X0 = X + t0 * TL_TT;
-      switch (dens) {
-        case DENS_TANH: tiled_launch<DENS_TANH>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
-        case DENS_EXP: tiled_launch<DENS_EXP>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
-        case DENS_CUBE: tiled_launch<DENS_CUBE>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
-        default: tiled_launch<DENS_LINEAR>(mode, nfp, ncp, dmu, alpha, t0, ntl, need_h, nsplit, nwg1, tpw, acc, X0); break;
+      switch (td) {
+        case DENS_TANH: tiled_launch<DENS_TANH>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
+        case DENS_EXP: tiled_launch<DENS_EXP>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
+        case DENS_CUBE: tiled_launch<DENS_CUBE>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
+        case DENS_TANH_S: tiled_launch<DENS_TANH_S>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
+        case DENS_EXP_S: tiled_launch<DENS_EXP_S>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
+        default: tiled_launch<DENS_LINEAR>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
       }
-      if (n_tiles == 0) break;
     }
     const size_t total = (size_t)(mode == 0 ? (need_h ? 2 : 1) * nc * nc : 0) + 3 * nc;
     k_reduce_tiled<<<(total + 255) / 256, 256, 0, stream>>>(d_slab, nsplit, d_trow, nwg1, ncp, (int)nc, need_h,
-                                                            mode == 1 ? 1 : 0, st, ks ? dens : -1, alpha,
-                                                            (double)n_local_);
-    HIP_OK(hipGetLastError());
-  }
-
-  void generic_eval(const double* w, size_t nc, const double* dmu, int dens, double alpha, bool need_h, double* st) {
-    const uint64_t CH = 1ull << 16;
-    const int splits = 16;
-    const size_t nsq = nc * nc;
-    double* dw = ensure(d_w, cap_w, nc * nf);
-    HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    // chunk scratch: Y, ψ, ψ′, ℓ (nc × CH each) + slabs + row sums
-    const size_t need = 4 * nc * CH + (need_h ? 2 : 1) * splits * nsq + 3 * nc;
-    double* base = ensure(d_chunk, cap_chunk, need);
-    double *Y = base, *P = Y + nc * CH, *D = P + nc * CH, *L = D + nc * CH;
-    double* gsl = L + nc * CH;
-    double* hsl = gsl + splits * nsq;
-    double* rs = hsl + (need_h ? splits * nsq : 0);
-    HIP_OK(hipMemsetAsync(gsl, 0, ((need_h ? 2 : 1) * splits * nsq + 3 * nc) * sizeof(double), stream));
-    const int tiles = (int)((nc + 63) / 64);
-    for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
-      const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
-      const uint64_t g = (cn + 255) / 256;
-      switch (dens) {
-        case DENS_TANH: k_ycomp<DENS_TANH><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
-        case DENS_EXP: k_ycomp<DENS_EXP><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
-        case DENS_CUBE: k_ycomp<DENS_CUBE><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
-        default: k_ycomp<DENS_LINEAR><<<g, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, alpha, c0, cn, Y, CH, P, D, L, CH); break;
-      }
-      HIP_OK(hipGetLastError());
-      k_gemm_nt<false><<<tiles * tiles * splits, 256, 0, stream>>>(P, Y, CH, (int)nc, cn, splits, gsl);
-      if (need_h) k_gemm_nt<true><<<tiles * tiles * splits, 256, 0, stream>>>(D, Y, CH, (int)nc, cn, splits, hsl);
-      k_rowsums_chunk<<<dim3((unsigned)nc, 3), 256, 0, stream>>>(D, L, Y, CH, CH, cn, cn, rs, (int)nc);
-      HIP_OK(hipGetLastError());
-    }
-    k_sum_slabs<<<(nsq + 255) / 256, 256, 0, stream>>>(gsl, splits, nsq, st);
-    if (need_h) k_sum_slabs<<<(nsq + 255) / 256, 256, 0, stream>>>(hsl, splits, nsq, st + nsq);
-    HIP_OK(hipMemcpyAsync(st + (need_h ? 2 : 1) * nsq, rs, 3 * nc * sizeof(double), hipMemcpyDeviceToDevice, stream));
+                                                            mode == 1 ? 1 : 0, st, td, alpha, (double)n_local_);
     HIP_OK(hipGetLastError());
   }
 
@@ -2841,20 +2744,38 @@ struct DeviceCtx : Evaluator {
 
   void sources(const double* w, size_t nc, const double* mu, double* out) override {
     HIP_OK(hipSetDevice(device));
-    double* dw = ensure(d_w, cap_w, nc * nf);
-    HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    const double* dmu = resident_mu(mu);  // null: X is centred in place
+    resident_mu(mu);  // X is centred in place: Y = W·X
+    ystore_upload(w, nc, nf);
     const uint64_t CH = 1ull << 20;
     double* Y = ensure(d_chunk, cap_chunk, nc * CH);
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
       const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
-      k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, 0.0, c0,
-                                                               cn, Y, CH, nullptr, nullptr, nullptr, 0);
-      HIP_OK(hipGetLastError());
+      ystore_run(X + c0, ldx, nf, nc, cn, Y, CH);
       HIP_OK(hipMemcpy2DAsync(out + c0, n_local_ * sizeof(double), Y, CH * sizeof(double), cn * sizeof(double), nc,
                               hipMemcpyDeviceToHost, stream));
     }
     HIP_OK(hipStreamSynchronize(stream));
+  }
+
+  // Sources kept in HBM (S = W·(X − μ), nc × ldx, row-major, zero padding past
+  // n_local): the whole shard in one k_ystore pass — for callers that consume
+  // the sources on the device; *kernel_ms = the pass's HIP-event time.
+  double* d_src = nullptr; size_t cap_src = 0;
+  const double* sources_resident(const double* w, size_t nc, const double* mu, double* kernel_ms) {
+    HIP_OK(hipSetDevice(device));
+    resident_mu(mu);
+    ystore_upload(w, nc, nf);
+    double* S = ensure(d_src, cap_src, nc * ldx);
+    if (ldx > n_local_)  // the padding columns read as zero, like X's
+      HIP_OK(hipMemset2DAsync(S + n_local_, ldx * sizeof(double), 0, (ldx - n_local_) * sizeof(double), nc, stream));
+    HIP_OK(hipEventRecord(ev[1], stream));
+    ystore_run(X, ldx, nf, nc, n_local_, S, ldx);
+    HIP_OK(hipEventRecord(ev[2], stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    float a = 0;
+    HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2]));
+    if (kernel_ms) *kernel_ms = a;
+    return S;
   }
 
   // JADE sweeps as one cooperative launch (jade_sweeps.inc): the np cumulant
@@ -2932,9 +2853,8 @@ struct DeviceCtx : Evaluator {
       for (int i = 0; i < (int)nc; ++i)
         for (int j = i; j < (int)nc; ++j) { pi[q] = i; pj[q] = j; ++q; }
     }
-    double* dw = ensure(d_w, cap_w, nc * nf);
-    HIP_OK(hipMemcpyAsync(dw, w, nc * nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    const double* dmu = resident_mu(mu);  // null: X is centred in place
+    resident_mu(mu);  // X is centred in place: Y = W·X
+    ystore_upload(w, nc, nf);
     const bool mfma_path = nc <= 64;  // larger nc: the VALU tile kernel
     const uint64_t CH = mfma_path ? (1ull << 22) : (1ull << 16);
     // tiles of the upper triangle and the T split (≈ whole rounds of one workgroup per CU)
@@ -2963,8 +2883,7 @@ struct DeviceCtx : Evaluator {
     bool first = true;
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
       const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
-      k_ycomp<DENS_NONE><<<(cn + 255) / 256, 256, 0, stream>>>(X, ldx, n_local_, (int)nf, (int)nc, dw, dmu, 0.0, c0,
-                                                               cn, Y, CH, nullptr, nullptr, nullptr, 0);
+      ystore_run(X + c0, ldx, nf, nc, cn, Y, CH);
       if (mfma_path) {
         const uint64_t nsb = (cn + 15) / 16;
         const uint64_t spb = (nsb + nsplit - 1) / nsplit;
@@ -3000,6 +2919,12 @@ void device_ctx_generate(Evaluator* e, uint64_t nf, uint64_t nt, uint64_t seed, 
   static_cast<DeviceCtx*>(e)->generate(nf, nt, seed, a_out);
 }
 void device_ctx_download(Evaluator* e, double* out) { static_cast<DeviceCtx*>(e)->download(out); }
+const double* device_ctx_sources_resident(Evaluator* e, const double* w, size_t nc, const double* mu, double* ms,
+                                          uint64_t* ld) {
+  auto* d = static_cast<DeviceCtx*>(e);
+  *ld = d->ldx;
+  return d->sources_resident(w, nc, mu, ms);
+}
 uint64_t device_ctx_t0(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->t0; }
 void device_ctx_timing(const Evaluator* e, double* k, double* c) {
   auto* d = static_cast<const DeviceCtx*>(e);
