@@ -204,6 +204,7 @@ def main():
 
     iters_to_tol, converged, total_passes = None, None, None
     t_tol = None
+    transform = None
     if args.to_tol:
         t1 = time.perf_counter()
         while not done:
@@ -211,6 +212,18 @@ def main():
         t_tol = time.perf_counter() - t1
         res = solver.finish()
         iters_to_tol, converged, total_passes = res.n_iterations, res.converged, res.n_evaluations
+        # Picard.transform (solver.rs:199-214) of this shard kept in HBM: S = W_full·(X − μ)
+        # in one k_ystore pass (2·N²·T flop, 8·N·T bytes read + 8·N·T written)
+        wf = res.full_unmixing()
+        tr_ms = [ctx.sources_device(wf, res.mean)[2] for _ in range(3)]
+        tl = ctx.n_local
+        ms_tr = sum(tr_ms) / len(tr_ms)
+        transform = {"kernel": "k_ystore<32>", "avg_kernel_ms": ms_tr, "launches": len(tr_ms),
+                     "achieved_tflops": 2.0 * n * n * tl / (ms_tr * 1e-3) / 1e12,
+                     "frac_mfma": 2.0 * n * n * tl / (ms_tr * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                     "hbm_gbs_algorithmic": 16.0 * n * tl / (ms_tr * 1e-3) / 1e9,
+                     "bound_ms": max(2.0 * n * n * tl / (FP64_MFMA_PEAK_TFLOPS * 1e12),
+                                     16.0 * n * tl / (HBM_PEAK_GBS * 1e9)) * 1e3}
 
     if rank != 0:
         return
@@ -270,6 +283,7 @@ def main():
                                  "avg_ms": (v[0] / v[1]) if v[1] else None} for k, v in brk.items()},
         "roofline": roof,
         "roofline_kernels": rooflines,
+        "transform": transform,
         "timings_s": {"generate": t_gen, "setup": t_setup, "to_tol_untimed": t_tol},
     }
     if args.cpu_baseline and world == 1:

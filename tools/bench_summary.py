@@ -16,3 +16,7 @@ for k, c in (d.get("other_configs") or {}).items():
         k, c["workload"], c["iters_to_tol"], c["setup_s"], c["iterations_s"], c["samples_per_s_per_iter"],
         c["passes"], c["amari_vs_true_mixing"]))
     print("      kernel ms", c["kernel_ms"], "launches", c["kernel_launches"])
+if d.get("transform"):
+    t = d["transform"]
+    print("  transform %s %.2f ms  %.1f TF/s (%.3f of MFMA peak)  %.0f GB/s  bound %.2f ms" % (
+        t["kernel"], t["avg_kernel_ms"], t["achieved_tflops"], t["frac_mfma"], t["hbm_gbs_algorithmic"], t["bound_ms"]))
