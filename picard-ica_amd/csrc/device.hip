@@ -1080,6 +1080,34 @@ __host__ __device__ inline size_t tl_frag(uint64_t tt, int ib, int ts, int r, in
   return ((((size_t)tt * nib + ib) * TL_TS + ts) * 4 + r) * 64;
 }
 
+// End-of-block barrier of the store-epilogue kernels (k_ystore, k_tiled_yw):
+// waits for this wave's LDS-DMA of the next block — issued BEFORE the block's
+// NST global stores — but not for the stores themselves. vmcnt counts loads,
+// stores and LDS-DMA together in issue order (MI355X_MICROARCH.md 's_waitcnt
+// vmcnt(N)'), and __syncthreads() drains it to 0, which put every block's
+// store round trip on the critical path. NST must be the exact number of
+// vector-memory instructions this wave issued after its DMA (0 drains all).
+template <int NST>
+__device__ __forceinline__ void dma_barrier() {
+  static_assert(NST >= 0 && NST < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// XCD-aware decode of a 1D grid into (sample range x, role): blocks b and b + 8
+// land on one XCD (round-robin dispatch; MI355X_MICROARCH.md "Workgroup
+// dispatch"), so the nroles roles of range x are consecutive slots of ONE XCD,
+// start together and share that XCD's L2: X (or the fragments) is fetched from
+// HBM once per range instead of once per role. Placement is a speed matter
+// only; the grid is 8·⌈nx/8⌉·nroles blocks and those with x ≥ nx exit at once.
+__device__ __forceinline__ bool xcd_decode(int nroles, uint64_t nx, uint64_t& x, int& role) {
+  const unsigned i = blockIdx.x, slot = i >> 3;
+  role = (int)(slot % (unsigned)nroles);
+  x = (uint64_t)(slot / (unsigned)nroles) * 8 + (i & 7);
+  return x < nx;
+}
+__host__ inline unsigned xcd_grid(uint64_t nx, int nroles) { return (unsigned)((nx + 7) / 8 * 8 * nroles); }
+
 // Phase 1 with W in registers: the workgroup role blockIdx.y owns output rows
 // [128·role, 128·role + 128); wave w owns row block ib = 8·role + w and keeps
 // its W fragment (16 rows × 4·KS features of this chunk) in VGPRs for the whole
@@ -1090,18 +1118,21 @@ __host__ __device__ inline size_t tl_frag(uint64_t tt, int ib, int ts, int r, in
 // MODE 0: y, ψ (, ψ′) fragments + all row terms; 1: Σℓ, Σy² terms only;
 // 2: partial y of a feature chunk only. yin (MODE 0/1/2, may alias ybuf): the
 // partial y of the earlier feature chunks, added at the start of each chain.
-template <int KS, int DENS, int MODE>
+template <int KS, int DENS, int MODE, bool YIN>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, int ncp,
            const double* __restrict__ WpT, const double* __restrict__ mu, double alpha, uint64_t bpw,
            uint64_t n_blocks, double* __restrict__ partials, int accumulate, double* ybuf,
-           double* __restrict__ pbuf, double* __restrict__ dbuf, const double* yin) {
+           double* __restrict__ pbuf, double* __restrict__ dbuf, const double* yin, uint64_t nwgx) {
   constexpr int NFP = 4 * KS, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave per block
   static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int nib = ncp / 16;
-  const int ib = blockIdx.y * 8 + wave;
+  uint64_t wx;
+  int role;
+  if (!xcd_decode((nib + 7) / 8, nwgx, wx, role)) return;
+  const int ib = role * 8 + wave;
   const bool active = ib < nib;
   const int row = ib * 16 + lr;
   const double alpha_ = alpha, inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
@@ -1113,7 +1144,7 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) wf[ks] = active ? WpT[(size_t)(4 * ks + lk) * ncp + row] : 0.0;
   RowAcc racc;
-  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_begin = wx * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   // X staged by LDS-DMA (the centred resident X: μ = null; samples past n_in are
   // the zero padding of X, rows ≥ nf read row 0 against zero W columns): wave w
@@ -1137,15 +1168,16 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
     __syncthreads();
     int cur = 0;
     for (uint64_t b = b_begin; b < b_end; ++b) {
-      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
-      if (active) {
-        const uint64_t tt = b >> 2;
-        const int ts = (int)(b & 3);
-        const size_t f0 = tl_frag(tt, ib, ts, 0, nib) + lane;
-        d4 yv = d4{0, 0, 0, 0};
-        if (yin)
+      const size_t f0 = tl_frag(b >> 2, ib, (int)(b & 3), 0, nib) + lane;
+      d4 yv = d4{0, 0, 0, 0};
+      // partial y of the earlier feature chunks, loaded BEFORE the DMA so the wait
+      // for it leaves the DMA in flight (a load issued after it drained both)
+      if (YIN && active)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) yv[r] = yin[f0 + 64 * r];
+        for (int r = 0; r < 4; ++r) yv[r] = yin[f0 + 64 * r];
+      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
+      __builtin_amdgcn_sched_barrier(0);  // the DMA stays ahead of this block's stores (dma_barrier)
+      if (active) {
         const double* xrow = xs0 + cur * XS + lk * 16 + lr;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) yv = mfma(xrow[(4 * ks) * 16], wf[ks], yv);
@@ -1167,7 +1199,11 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
         if constexpr (MODE != 2)
           if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc);
       }
-      __syncthreads();  // also waits for this wave's LDS-DMA of block b + 1
+      // this wave's LDS-DMA of block b + 1 landed; its y / ψ (/ ψ′) stores may still be in flight
+      if (!active || MODE == 1) dma_barrier<0>();
+      else if (MODE == 2) dma_barrier<4>();
+      else if (dbuf) dma_barrier<12>();
+      else dma_barrier<8>();
       cur ^= 1;
     }
   }
@@ -1180,7 +1216,7 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   rs_l += __shfl_xor(rs_l, 16); rs_l += __shfl_xor(rs_l, 32);
   rs_q += __shfl_xor(rs_q, 16); rs_q += __shfl_xor(rs_q, 32);
   if (active && lk == 0) {
-    double* out = partials + (size_t)blockIdx.x * 3 * ncp;
+    double* out = partials + (size_t)wx * 3 * ncp;
     const double v[3] = {MODE == 0 ? rs_d : 0.0, rs_l, rs_q};
 #pragma unroll
     for (int c = 0; c < 3; ++c) out[c * ncp + row] = accumulate ? out[c * ncp + row] + v[c] : v[c];
@@ -1194,11 +1230,16 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
 // or 4 waves — with the next sub-block prefetched into registers a full
 // iteration ahead; one barrier per sub-block. Wave (gi, gj) accumulates a 64×32
 // patch of G (and H) in registers.
-template <bool NEED_H>
+// DFROMP (tanh, α > 0): ψ′ = α(1 − ψ²) is formed here from the staged ψ — the
+// expression density_acc4 evaluates, so the same bits — instead of being
+// written by phase 1 and read back (one array less each way).
+template <bool NEED_H, bool DFROMP>
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
 k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, const double* __restrict__ dbuf,
-              int ncp, uint64_t n_tiles, uint64_t tps, double* __restrict__ slabs, int accumulate) {
-  constexpr int NARR = NEED_H ? 3 : 2;  // staged arrays: ψ, y (, ψ′)
+              int ncp, uint64_t n_tiles, uint64_t tps, double* __restrict__ slabs, int accumulate, double alpha,
+              uint64_t nsplit) {
+  static_assert(NEED_H || !DFROMP, "ψ′ only feeds H");
+  constexpr int NARR = NEED_H && !DFROMP ? 3 : 2;  // staged arrays: ψ, y (, ψ′)
   constexpr int SUB = 8 * 256;          // doubles per array per sub-block (8 row blocks × 4 r × 64)
   constexpr int PRE = NARR * SUB / 2 / FUSED_THREADS;  // 2 slots per array
   static_assert(SUB == 4 * FUSED_THREADS, "slot map assumes 512 threads");
@@ -1206,7 +1247,10 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
   const int lr = lane & 15, lk = lane >> 4;
   const int nib = ncp / 16;
   const int nto = (nib + 7) / 8;
-  const int ti = blockIdx.x / nto, tj = blockIdx.x % nto;
+  uint64_t split;
+  int tile;  // the nto² output tiles of one T split share an XCD: ψ / y fragments come from its L2
+  if (!xcd_decode(nto * nto, nsplit, split, tile)) return;
+  const int ti = tile / nto, tj = tile % nto;
   const int gi0 = (wave >> 2) * 4, gj0 = (wave & 3) * 2;  // local row blocks
   extern __shared__ double smem[];
   double* lds = smem;  // [2][NARR][8][4][64]
@@ -1227,7 +1271,7 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
     ok[p] = gb < nib;
     soff[p] = (ok[p] ? gb : 0) * 1024 + off;  // + ((tt·nib)·4 + ts)·256 per sub-block
   }
-  const uint64_t t_begin = (uint64_t)blockIdx.y * tps;
+  const uint64_t t_begin = split * tps;
   const uint64_t t_end = t_begin + tps < n_tiles ? t_begin + tps : n_tiles;
   const uint64_t s_begin = t_begin * 4, s_end = t_end * 4;  // sub-blocks
   double2 pre[PRE];
@@ -1258,7 +1302,8 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           pa[i] = img[((gi0 + i) * 4 + r) * 64 + lane];
-          if constexpr (NEED_H) da[i] = img[2 * SUB + ((gi0 + i) * 4 + r) * 64 + lane];
+          if constexpr (DFROMP) da[i] = alpha * __builtin_fma(-pa[i], pa[i], 1.0);
+          else if constexpr (NEED_H) da[i] = img[2 * SUB + ((gi0 + i) * 4 + r) * 64 + lane];
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) yb[j] = img[SUB + ((gj0 + j) * 4 + r) * 64 + lane];
@@ -1277,7 +1322,7 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
     }
   }
   const size_t nsq = (size_t)ncp * ncp;
-  double* slab = slabs + (size_t)blockIdx.y * (NEED_H ? 2 : 1) * nsq;
+  double* slab = slabs + (size_t)split * (NEED_H ? 2 : 1) * nsq;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1435,14 +1480,17 @@ __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf, int ncp,
               const double* __restrict__ WpT, const double* __restrict__ ZpT, const double* __restrict__ mu,
               double alpha, const double* __restrict__ alphas, int na, uint64_t bpw, uint64_t n_blocks,
-              double* __restrict__ partials) {
+              double* __restrict__ partials, uint64_t nwgx) {
   constexpr int NFP = 4 * KS, KH = KS / 2, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave
   static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const int nib = ncp / 16;
   const int rb = wave & 3, kh = wave >> 2;
-  const int ib = blockIdx.y * 4 + rb;
+  uint64_t wx;
+  int role;
+  if (!xcd_decode((nib + 3) / 4, nwgx, wx, role)) return;
+  const int ib = role * 4 + rb;
   const bool active = ib < nib;
   const int row = ib * 16 + lr;
   const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
@@ -1464,7 +1512,7 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
 #pragma unroll
   for (int u = 0; u < ML2_TRIES; ++u) aj[u] = (kh + 2 * u < na) ? alphas[kh + 2 * u] : 0.0;
   const int my_na = na > kh ? (na - kh + 1) / 2 : 0;
-  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_begin = wx * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint64_t b_last = b_end - 1;
   // X staged by LDS-DMA as in k_tiled_yw (centred resident X, μ = null)
@@ -1528,7 +1576,7 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
     }
   }
   // partials: [ML_NA][2][ncp] raw (Σℓ term, Σy²) per try
-  double* out = partials + (size_t)blockIdx.x * ML_NA * 2 * ncp;
+  double* out = partials + (size_t)wx * ML_NA * 2 * ncp;
 #pragma unroll
   for (int u = 0; u < ML2_TRIES; ++u) {
     if (u < my_na) {
@@ -1607,15 +1655,19 @@ __global__ void __launch_bounds__(256) k_reduce(const double* __restrict__ parti
 template <int KS>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_ystore(const double* __restrict__ X, uint64_t ldx, int nrows_x, const double* __restrict__ WpT, int ncp, int nc,
-         uint64_t n_out, uint64_t bpw, uint64_t n_blocks, double* __restrict__ Y, uint64_t ldy, int accumulate) {
+         uint64_t n_out, uint64_t bpw, uint64_t n_blocks, double* __restrict__ Y, uint64_t ldy, int accumulate,
+         uint64_t nwgx) {
   constexpr int NFP = 4 * KS, XS = 16 * NFP, NU = NFP / 64;  // LDS-DMA instructions per wave per block
   static_assert(NFP % 64 == 0, "8 waves × 8 rows per instruction");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
-  const int ib = blockIdx.y * 8 + wave;
+  uint64_t wx;
+  int role;
+  if (!xcd_decode((ncp / 16 + 7) / 8, nwgx, wx, role)) return;
+  const int ib = role * 8 + wave;
   const bool active = ib < ncp / 16;
   extern __shared__ double smem[];
-  double* xs0 = smem;  // [2][NFP][16]
+  double* xs0 = smem;  // [2 buffers][2 blocks][NFP][16]
   double wf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) wf[ks] = active ? WpT[(size_t)(4 * ks + lk) * ncp + ib * 16 + lr] : 0.0;
@@ -1631,31 +1683,57 @@ k_ystore(const double* __restrict__ X, uint64_t ldx, int nrows_x, const double* 
       __builtin_amdgcn_global_load_lds((gbl_vptr)(src[u] + b * 16),
                                        (lds_vptr)(xs + (wave * (NFP / 8) + 8 * u) * 16), 16, 0, 0);
   };
-  const uint64_t b_begin = (uint64_t)blockIdx.x * bpw;
+  const uint64_t b_begin = wx * bpw;
   const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   if (b_begin >= b_end) return;
-  stage(b_begin, xs0);
+  // blocks in pairs: two independent MFMA chains and one barrier per 32 samples
+  auto stage2 = [&](uint64_t b0, double* xs) {
+    stage(b0, xs);
+    if (b0 + 1 < b_end) stage(b0 + 1, xs + XS);
+  };
+  stage2(b_begin, xs0);
   __syncthreads();
   int cur = 0;
-  for (uint64_t b = b_begin; b < b_end; ++b) {
-    if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * XS);
+  for (uint64_t b0 = b_begin; b0 < b_end; b0 += 2) {
+    if (b0 + 2 < b_end) stage2(b0 + 2, xs0 + (cur ^ 1) * 2 * XS);
+    __builtin_amdgcn_sched_barrier(0);  // the DMA stays ahead of this pair's stores (dma_barrier)
     if (active) {
-      d4 yv = d4{0, 0, 0, 0};
-      const double* xrow = xs0 + cur * XS + lk * 16 + lr;
+      d4 ya = d4{0, 0, 0, 0}, yb = d4{0, 0, 0, 0};  // yb: stale LDS when the pair is cut short (not stored)
+      const double* xrow = xs0 + cur * 2 * XS + lk * 16 + lr;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) yv = mfma(wf[ks], xrow[(4 * ks) * 16], yv);
-      const uint64_t t = b * 16 + lr;
-      if (t < n_out)
+      for (int ks = 0; ks < KS; ++ks) {
+        ya = mfma(wf[ks], xrow[(4 * ks) * 16], ya);
+        yb = mfma(wf[ks], xrow[XS + (4 * ks) * 16], yb);
+      }
+      const uint64_t t = b0 * 16 + lr;
+      // both 16 × 16 tiles inside Y and no read-back: exactly 8 stores after the DMA
+      if (!accumulate && b0 * 16 + 32 <= n_out && ib * 16 + 16 <= nc) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = ib * 16 + lk + 4 * r;
-          if (row < nc) {
-            double* p = Y + (size_t)row * ldy + t;
-            *p = accumulate ? *p + yv[r] : yv[r];
-          }
+          double* p = Y + (size_t)(ib * 16 + lk + 4 * r) * ldy + t;
+          p[0] = ya[r];
+          p[16] = yb[r];
         }
+        dma_barrier<8>();
+        cur ^= 1;
+        continue;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t th = t + 16 * h;
+        if (th < n_out)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = ib * 16 + lk + 4 * r;
+            if (row < nc) {
+              double* p = Y + (size_t)row * ldy + th;
+              const double v = h ? yb[r] : ya[r];
+              *p = accumulate ? *p + v : v;
+            }
+          }
+      }
     }
-    __syncthreads();  // also waits for this wave's LDS-DMA of block b + 1
+    dma_barrier<0>();  // edge tiles / inactive waves: drain everything
     cur ^= 1;
   }
 }
@@ -2023,19 +2101,20 @@ struct DeviceCtx : Evaluator {
     static bool attr = false;
     if (!attr) {
       HIP_OK(hipFuncSetAttribute((const void*)k_ystore<KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 2 * 16 * 4 * KS * (int)sizeof(double)));
+                                 4 * 16 * 4 * KS * (int)sizeof(double)));
       attr = true;
     }
     const uint64_t n_blocks = (n_out + 15) / 16;
     const int nroles = (ncp / 16 + 7) / 8;
-    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(n_blocks, (uint64_t)2 * n_cu / nroles + 1));
-    const uint64_t bpw = (n_blocks + want - 1) / want;
+    // two workgroups per CU in ONE round (a 2·n_cu + 1-th would run alone afterwards)
+    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(n_blocks, std::max(1, 2 * n_cu / nroles)));
+    const uint64_t bpw = ((n_blocks + want - 1) / want + 1) & ~uint64_t(1);  // whole block pairs
     const unsigned nwg = (unsigned)((n_blocks + bpw - 1) / bpw);
     constexpr int CHK = 4 * KS;
     for (uint64_t k0 = 0; k0 < nrows; k0 += CHK)
-      k_ystore<KS><<<dim3(nwg, nroles), FUSED_THREADS, (size_t)2 * 16 * CHK * sizeof(double), stream>>>(
+      k_ystore<KS><<<xcd_grid(nwg, nroles), FUSED_THREADS, (size_t)4 * 16 * CHK * sizeof(double), stream>>>(
           Xs + k0 * lds, lds, (int)std::min<uint64_t>(CHK, nrows - k0), dwt + k0 * ncp, ncp, (int)nc, n_out, bpw,
-          n_blocks, Y, ldy, k0 > 0 ? 1 : 0);
+          n_blocks, Y, ldy, k0 > 0 ? 1 : 0, (uint64_t)nwg);
     HIP_OK(hipGetLastError());
   }
   // Wᵀ (zero-padded to whole chunks and row blocks) into d_wys, once per map
@@ -2271,8 +2350,8 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
       attr[want_y2] = true;
     }
-    k<<<dim3(nwg, nroles), FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, ncp, dw, dz, dmu, alpha, dal, na,
-                                                         bpw, n_blocks, part);
+    k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, ncp, dw, dz, dmu, alpha, dal, na,
+                                                             bpw, n_blocks, part, (uint64_t)nwg);
   }
   template <int D>
   void multi2_dispatch(int ks, int ncp, const double* dw, const double* dz, const double* dmu, double alpha,
@@ -2394,14 +2473,20 @@ struct DeviceCtx : Evaluator {
     const uint64_t bpw = (n_blocks + nwg1 - 1) / nwg1;
     const int nroles = (ncp / 16 + 7) / 8;
     const size_t lds = (size_t)2 * 16 * 4 * KS * sizeof(double);
-    auto k = mode == 0 ? k_tiled_yw<KS, D, 0> : mode == 1 ? k_tiled_yw<KS, D, 1> : k_tiled_yw<KS, D, 2>;
-    static bool attr[3] = {false, false, false};
-    if (!attr[mode]) {
+    // partial y of earlier feature chunks (yin) only exists above 4·KS = 256 features
+    constexpr bool YC = KS == 64;
+    auto k = yin && YC ? (mode == 0 ? k_tiled_yw<KS, D, 0, YC> : mode == 1 ? k_tiled_yw<KS, D, 1, YC> : k_tiled_yw<KS, D, 2, YC>)
+                       : (mode == 0 ? k_tiled_yw<KS, D, 0, false> : mode == 1 ? k_tiled_yw<KS, D, 1, false>
+                                                                             : k_tiled_yw<KS, D, 2, false>);
+    if (yin && !YC) throw computation_error("tiled pass: feature chunks need KS = 64");
+    static bool attr[2][3] = {{false, false, false}, {false, false, false}};
+    if (!attr[yin != nullptr][mode]) {
       HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
-      attr[mode] = true;
+      attr[yin != nullptr][mode] = true;
     }
-    k<<<dim3(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, 0, (int)nrows, ncp, wpt, nullptr, alpha, bpw,
-                                                          n_blocks, d_trow, acc ? 1 : 0, yb, pb, db, yin);
+    k<<<xcd_grid(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, 0, (int)nrows, ncp, wpt, nullptr, alpha, bpw,
+                                                              n_blocks, d_trow, acc ? 1 : 0, yb, pb, db, yin,
+                                                              (uint64_t)nwg1);
   }
   template <int D>
   void yw_launch(int ks, int mode, int ncp, double alpha, uint64_t ntl, int nwg1, bool acc, const double* X0,
@@ -2418,9 +2503,10 @@ struct DeviceCtx : Evaluator {
   void tiled_launch(int mode, int ks, int ncp, double alpha, uint64_t ntl, bool need_h, int nsplit, int nwg1, bool acc,
                     const double* X0) {
     const size_t chunk = (size_t)ncp * ntl * TL_TT;
+    constexpr bool dfromp = D == DENS_TANH;  // ψ′ = α(1 − ψ²) formed in phase 2
     double* yb = d_tbuf;
     double* pb = d_tbuf + chunk;
-    double* db = need_h ? d_tbuf + 2 * chunk : nullptr;
+    double* db = need_h && !dfromp ? d_tbuf + 2 * chunk : nullptr;
     const uint64_t kc = 4 * (uint64_t)ks;  // features per chunk
     for (uint64_t k0 = 0; k0 < nf; k0 += kc) {
       const bool last = k0 + kc >= nf;
@@ -2431,14 +2517,15 @@ struct DeviceCtx : Evaluator {
     if (mode == 0) {
       const int nto = (ncp / 16 + 7) / 8;
       const uint64_t tps = (ntl + nsplit - 1) / nsplit;
-      const size_t lds2 = (size_t)2 * (need_h ? 3 : 2) * 8 * 256 * sizeof(double);
+      const size_t lds2 = (size_t)2 * (db ? 3 : 2) * 8 * 256 * sizeof(double);
       static bool attr2[2] = {false, false};
-      auto k2 = need_h ? k_tiled_gram2<true> : k_tiled_gram2<false>;
+      auto k2 = !need_h ? k_tiled_gram2<false, false> : dfromp ? k_tiled_gram2<true, true> : k_tiled_gram2<true, false>;
       if (!attr2[need_h]) {
         HIP_OK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr2[need_h] = true;
       }
-      k2<<<dim3(nto * nto, nsplit), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0);
+      k2<<<xcd_grid(nsplit, nto * nto), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0,
+                                                                       alpha, (uint64_t)nsplit);
       HIP_OK(hipGetLastError());
     }
   }
@@ -2463,15 +2550,16 @@ struct DeviceCtx : Evaluator {
       const double have = (double)fr + (double)cap_tbuf * sizeof(double) - 16e9;
       tiled_budget_ = std::max(24e9, std::min(have, 0.6 * (double)tot));
     }
+    const double narr = need_h && tiled_dens(dens, alpha) != DENS_TANH ? 3.0 : 2.0;  // y, ψ (, ψ′)
     const uint64_t max_tiles =
-        std::max<uint64_t>(1, (uint64_t)(tiled_budget_ / (3.0 * ncp * TL_TT * sizeof(double))));
+        std::max<uint64_t>(1, (uint64_t)(tiled_budget_ / (narr * ncp * TL_TT * sizeof(double))));
     const uint64_t ct = std::min<uint64_t>(std::max<uint64_t>(n_tiles, 1), max_tiles);
     const int nroles = (ncp / 16 + 7) / 8;
     const int nwg1 = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)n_cu * 2 / nroles, ct * 4));
     const int nto = (ncp / 16 + 7) / 8;
     const int nsplit = (int)std::max<uint64_t>(1, std::min<uint64_t>(ct, (uint64_t)(2 * n_cu / (nto * nto))));
     // y buffer: always in mode 0; in mode 1 only to carry partial y across feature chunks
-    if (mode == 0) ensure(d_tbuf, cap_tbuf, (size_t)(need_h ? 3 : 2) * ncp * ct * TL_TT);
+    if (mode == 0) ensure(d_tbuf, cap_tbuf, (size_t)narr * ncp * ct * TL_TT);
     else if (nf > kc) ensure(d_tbuf, cap_tbuf, (size_t)ncp * ct * TL_TT);
     if (mode == 0) ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
     ensure(d_trow, cap_trow, (size_t)nwg1 * 3 * ncp);

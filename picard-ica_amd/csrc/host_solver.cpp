@@ -228,7 +228,8 @@ static double now_ms() {
 
 void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
-  ev_->want_y2 = !cfg_.ortho;  // Σy² is read only by the non-orthogonal step / extended loss
+  // Σy² is read only by the extended non-orthogonal loss and Hessian (core.rs:79-81, :251)
+  ev_->want_y2 = !cfg_.ortho && extended_;
   const double t0 = now_ms();
   ev_->eval(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
   eval_ms_ += now_ms() - t0;
@@ -238,7 +239,7 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
 
 bool Solver::evaluate_loss(const Mat& w_core, EvalStats* out) {
   Mat wt = matmul(w_core, P_);
-  ev_->want_y2 = !cfg_.ortho;
+  ev_->want_y2 = !cfg_.ortho && extended_;
   const double t0 = now_ms();
   const bool partial =
       ev_->eval_loss(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out, keep_y_);
