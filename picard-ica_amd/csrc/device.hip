@@ -1831,24 +1831,38 @@ __global__ void __launch_bounds__(256) k_moments4(const double* __restrict__ Y, 
     }
 }
 
-// Fourth moments for JADE on MFMA (jade.rs:91-113 as a Gram of pair products):
-// M4[p][q] = Σ_t z_p z_q, z_(i≤j) = y_i y_j. blockIdx.x = upper-triangle 128×128
-// output tile (tp ≤ tq), blockIdx.y = T split. Per 16-sample sub-block the Y
-// rows are staged in LDS, each thread forms 8 pair products straight into the
-// MFMA A/B fragment layout in LDS (every product feeds 2 or 4 waves), and wave
-// (gi, gj) accumulates a 64×32 patch; one barrier per sub-block. Slab s holds
-// split s's partial tile (summed in fixed order by k_moments4_reduce).
+// Fourth moments for JADE on MFMA (jade.rs:91-113 as a Gram of pair products).
+// Every entry of the np × np pair Gram M[(i,j)][(k,l)] = Σ_t y_i y_j y_k y_l is
+// one of the C(n+3, 4) distinct moments E[y_a y_b y_c y_d], a ≤ b ≤ c ≤ d, and
+// that moment is the Gram entry of ROW pair (a, b) and COLUMN pair (c, d) with
+// b ≤ c. So rows are ordered by their larger index (R: (a, b) ↦ b(b+1)/2 + a),
+// columns by their smaller one (C: (c, d) ↦ c·n − c(c−1)/2 + d − c), and only the
+// 128 × 128 (R, C) tiles that hold some b ≤ c are computed — 76 of the 289 at
+// n = 64, against 153 for the symmetric upper triangle; k_moments4_fill then
+// gathers the full lexicographic M the host expects.
+// 1D grid: block = tile·nsplit + split. Per 16-sample sub-block: the nc Y rows
+// land in LDS by LDS-DMA two sub-blocks ahead (segments XOR-swizzled per row so
+// the pair gathers below hit distinct banks), each thread forms 8 pair products
+// (masked past cn) into the MFMA A/B fragment image of the NEXT sub-block while
+// the waves run the MFMAs of this one (images double-buffered): one barrier per
+// sub-block. Wave (gi, gj) accumulates a 64 × 32 patch; slab s holds split s's
+// partial tile (summed in fixed order by k_moments4_reduce).
+__device__ __forceinline__ int m4_ys(int row, int t) {  // LDS index of Y(row, t) in a [64][16] sub-block
+  return row * 16 + ((((t >> 1) ^ (row & 7))) << 1) + (t & 1);
+}
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
-k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc, const int* __restrict__ pi,
-                const int* __restrict__ pj, int np, const int* __restrict__ tile_p, const int* __restrict__ tile_q,
-                uint64_t spb, double* __restrict__ slabs, size_t slab_stride) {
+k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc, const int* __restrict__ ri,
+                const int* __restrict__ rj, const int* __restrict__ ci, const int* __restrict__ cj, int np,
+                const int* __restrict__ tile_p, const int* __restrict__ tile_q, int nsplit, uint64_t spb,
+                double* __restrict__ slabs, size_t slab_stride) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
-  const int tp = tile_p[blockIdx.x], tq = tile_q[blockIdx.x];
+  const int tile = blockIdx.x / nsplit, split = blockIdx.x % nsplit;
+  const int tp = tile_p[tile], tq = tile_q[tile];
   const int gi0 = (wave >> 2) * 4, gj0 = (wave & 3) * 2;
   extern __shared__ double smem[];
-  double* ys = smem;              // [nc][16] Y sub-block
-  double* zf = smem + 64 * 16;    // [2 (P, Q)][8 pair blocks][4 k-steps][64 lanes]
+  double* ys0 = smem;              // [2][64][16] Y sub-blocks (swizzled)
+  double* zf0 = smem + 2 * 1024;   // [2][2 (P, Q)][8 pair blocks][4 k-steps][64 lanes]
   d4 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1862,41 +1876,54 @@ k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc,
     const int e = tid + FUSED_THREADS * u;
     const int set = e >> 11, blk = (e >> 8) & 7, ln = e & 63;
     const int pr = (set ? tq : tp) * 128 + blk * 16 + (ln & 15);
-    ia[u] = pr < np ? pi[pr] : -1;
-    ja[u] = pr < np ? pj[pr] : -1;
+    ia[u] = pr < np ? (set ? ci[pr] : ri[pr]) : -1;
+    ja[u] = pr < np ? (set ? cj[pr] : rj[pr]) : -1;
   }
   const uint64_t nsb = (cn + 15) / 16;
-  const uint64_t s_begin = blockIdx.y * spb, s_end = s_begin + spb < nsb ? s_begin + spb : nsb;
-  for (uint64_t sb = s_begin; sb < s_end; ++sb) {
-    for (int e = tid; e < nc * 16; e += FUSED_THREADS) {
-      const int r = e >> 4, c = e & 15;
-      const uint64_t t = sb * 16 + c;
-      ys[e] = t < cn ? Y[(size_t)r * ldy + t] : 0.0;
-    }
-    __syncthreads();
+  const uint64_t s_begin = (uint64_t)split * spb, s_end = s_begin + spb < nsb ? s_begin + spb : nsb;
+  // LDS-DMA: wave w moves rows 8w … 8w+7 of a sub-block (rows ≥ nc read row 0,
+  // never gathered); lane L → row 8w + L/8, slot L%8 holds segment (L%8) ^ (row%8)
+  const int yrow = 8 * wave + (lane >> 3);
+  const double* ysrc = Y + (size_t)(yrow < nc ? yrow : 0) * ldy + 2 * ((lane & 7) ^ (lane >> 3));
+  auto stage = [&](uint64_t sb, double* ys) {
+    __builtin_amdgcn_global_load_lds((gbl_vptr)(ysrc + sb * 16), (lds_vptr)(ys + wave * 128), 16, 0, 0);
+  };
+  auto products = [&](uint64_t sb, const double* ys, double* zf) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + FUSED_THREADS * u;
-      const int kk = (e >> 6) & 3, ln = e & 63;
-      const int t = 4 * kk + (ln >> 4);
-      zf[e] = ia[u] >= 0 ? ys[ia[u] * 16 + t] * ys[ja[u] * 16 + t] : 0.0;
+      const int t = 4 * ((e >> 6) & 3) + ((e & 63) >> 4);
+      zf[e] = ia[u] >= 0 && sb * 16 + t < cn ? ys[m4_ys(ia[u], t)] * ys[m4_ys(ja[u], t)] : 0.0;
     }
+  };
+  if (s_begin < s_end) {
+    stage(s_begin, ys0);
+    if (s_begin + 1 < s_end) stage(s_begin + 1, ys0 + 1024);
     __syncthreads();
+    products(s_begin, ys0, zf0);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t sb = s_begin; sb < s_end; ++sb) {
+      if (sb + 2 < s_end) stage(sb + 2, ys0 + cur * 1024);  // Y(sb) was read by the products of the last iteration
+      if (sb + 1 < s_end) products(sb + 1, ys0 + (cur ^ 1) * 1024, zf0 + (cur ^ 1) * 4096);
+      const double* zf = zf0 + cur * 4096;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      double a[4], b[2];
+      for (int kk = 0; kk < 4; ++kk) {
+        double a[4], b[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = zf[((gi0 + i) * 4 + kk) * 64 + lane];
+        for (int i = 0; i < 4; ++i) a[i] = zf[((gi0 + i) * 4 + kk) * 64 + lane];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = zf[2048 + ((gj0 + j) * 4 + kk) * 64 + lane];
+        for (int j = 0; j < 2; ++j) b[j] = zf[2048 + ((gj0 + j) * 4 + kk) * 64 + lane];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+      }
+      __syncthreads();  // products of sb + 1 written, this wave's DMA of sb + 2 landed
+      cur ^= 1;
     }
-    __syncthreads();
   }
-  double* out = slabs + blockIdx.y * slab_stride;
+  double* out = slabs + split * slab_stride;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1906,19 +1933,36 @@ k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc,
         const int p = tp * 128 + (gi0 + i) * 16 + lk + 4 * r, q = tq * 128 + (gj0 + j) * 16 + lr;
         if (p < np && q < np) out[(size_t)p * np + q] = acc[i][j][r];
       }
-  (void)lr;
 }
 
-// acc[p][q] (+)= Σ_s slabs[s][p][q] for the upper tiles written by k_moments4_mfma
+// acc[p][q] (+)= Σ_s slabs[s][p][q] over the (R, C) tiles k_moments4_mfma computed
 __global__ void k_moments4_reduce(const double* __restrict__ slabs, int nsplit, size_t slab_stride, int np,
-                                  int accumulate, double* __restrict__ acc) {
+                                  const unsigned char* __restrict__ tmask, int accumulate, double* __restrict__ acc) {
   const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (e >= (size_t)np * np) return;
-  const int p = (int)(e / np), q = (int)(e % np);
-  if (q / 128 < p / 128) return;  // lower tiles: not computed (mirrored on the host)
+  const int p = (int)(e / np), q = (int)(e % np), nt = (np + 127) / 128;
+  if (!tmask[(p / 128) * nt + q / 128]) return;
   double s = 0.0;
   for (int k = 0; k < nsplit; ++k) s += slabs[k * slab_stride + e];
   acc[e] = accumulate ? acc[e] + s : s;
+}
+
+// out[p][q] = M[(i,j)][(k,l)] in the lexicographic pair order (pi, pj) from the
+// (R, C) Gram: the sorted indices a ≤ b ≤ c ≤ d name the entry (R(a,b), C(c,d)).
+__global__ void k_moments4_fill(const double* __restrict__ acc, const int* __restrict__ pi, const int* __restrict__ pj,
+                                int n, int np, double* __restrict__ out) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= (size_t)np * np) return;
+  const int p = (int)(e / np), q = (int)(e % np);
+  int v[4] = {pi[p], pj[p], pi[q], pj[q]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)  // sort 4
+#pragma unroll
+    for (int j = 0; j < 3 - i; ++j)
+      if (v[j] > v[j + 1]) { const int t = v[j]; v[j] = v[j + 1]; v[j + 1] = t; }
+  const int r = v[1] * (v[1] + 1) / 2 + v[0];
+  const int c = v[2] * n - v[2] * (v[2] - 1) / 2 + (v[3] - v[2]);
+  out[e] = acc[(size_t)r * np + c];
 }
 
 // ---------------------------------------------------------------------------
@@ -2877,7 +2921,8 @@ struct DeviceCtx : Evaluator {
     const size_t mw = (np + n_cu - 1) / n_cu;
     const size_t G = (np + mw - 1) / mw;
     const size_t lds = (npos * mw + 4) * sizeof(double);
-    if (lds > 160 * 1024 || G > (size_t)n_cu || G > (size_t)JS_MAX_WG) return false;
+    if (lds > 160 * 1024 || G > (size_t)n_cu || G > (size_t)JS_MAX_WG || (n - 2) * mw > (size_t)JS_ROT_MAX * JS_THREADS)
+      return false;
     int coop = 0;
     HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
     if (!coop) return false;
@@ -2885,38 +2930,29 @@ struct DeviceCtx : Evaluator {
     int per_cu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_jade_sweeps, JS_THREADS, lds));
     if ((size_t)per_cu * n_cu < G) return false;
-    // [G][npos][mw]: workgroup g owns matrices g·mw … g·mw + mw − 1 (zero-padded)
-    std::vector<double> a_wg(G * npos * mw, 0.0);
-    for (size_t gg = 0; gg < G; ++gg)
-      for (size_t ps = 0; ps < npos; ++ps)
-        for (size_t j = 0; j < mw; ++j) {
-          const size_t m = gg * mw + j;
-          if (m < np) a_wg[(gg * npos + ps) * mw + j] = A[ps * np + m];
-        }
+    // A [npos][np] as the host built it; workgroup g loads matrices g·mw … g·mw + mw − 1
     std::vector<double> eye(n * n, 0.0);
     for (size_t i = 0; i < n; ++i) eye[i * n + i] = 1.0;
     double *d_a = nullptr, *d_v = nullptr, *d_g = nullptr;
     int* d_sw = nullptr;
-    unsigned* d_bar = nullptr;
-    HIP_OK(hipMalloc(&d_a, a_wg.size() * sizeof(double)));
+    HIP_OK(hipMalloc(&d_a, npos * np * sizeof(double)));
     HIP_OK(hipMalloc(&d_v, n * n * sizeof(double)));
-    HIP_OK(hipMalloc(&d_g, 2 * G * 3 * sizeof(double)));
+    HIP_OK(hipMalloc(&d_g, 2 * G * 3 * 2 * sizeof(double)));  // [2][3][G] granules {value, seq}
     HIP_OK(hipMalloc(&d_sw, 2 * sizeof(int)));
     const int theta_cap = (int)std::min<size_t>(max_iter / 10, 1u << 16);
     double* d_th = nullptr;
     HIP_OK(hipMalloc(&d_th, (theta_cap + 1) * sizeof(double)));
-    HIP_OK(hipMalloc(&d_bar, sizeof(unsigned)));
-    // the arrival counter starts at bar0 (0; PICARD_JADE_BAR_BASE presets it, e.g.
-    // just below 2^32, so a test can make the barrier targets wrap)
-    unsigned bar0 = 0;
-    if (const char* e = std::getenv("PICARD_JADE_BAR_BASE")) bar0 = (unsigned)std::strtoul(e, nullptr, 0);
+    // granule tags start at seq0 (0; PICARD_JADE_BAR_BASE presets it, a test hook:
+    // the sweeps must not depend on it)
+    unsigned long long seq0 = 0;
+    if (const char* e = std::getenv("PICARD_JADE_BAR_BASE")) seq0 = std::strtoull(e, nullptr, 0);
     long long max_pairs = (long long)std::min<size_t>(jade_max_pairs(), (size_t)LLONG_MAX);
-    HIP_OK(hipMemcpyAsync(d_bar, &bar0, sizeof(unsigned), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(d_a, a_wg.data(), a_wg.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemsetAsync(d_g, 0, 2 * G * 3 * 2 * sizeof(double), stream));  // tags 0 ≠ any seq ≥ seq0 + 1
+    HIP_OK(hipMemcpyAsync(d_a, A, npos * np * sizeof(double), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(d_v, eye.data(), n * n * sizeof(double), hipMemcpyHostToDevice, stream));
-    int n_i = (int)n, npos_i = (int)npos, mw_i = (int)mw, it_i = (int)std::min<size_t>(max_iter, 1u << 30);
+    int np_i = (int)np, n_i = (int)n, npos_i = (int)npos, mw_i = (int)mw, it_i = (int)std::min<size_t>(max_iter, 1u << 30);
     double tol_d = tol;
-    void* args[] = {&d_a, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_bar, &d_sw, &d_th, (void*)&theta_cap, &bar0, &max_pairs};
+    void* args[] = {&d_a, &np_i, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_sw, &d_th, (void*)&theta_cap, &seq0, &max_pairs};
     HIP_OK(hipLaunchCooperativeKernel((const void*)k_jade_sweeps, dim3((unsigned)G), dim3(JS_THREADS), args,
                                       (unsigned)lds, stream));
     int sw[2] = {0, 0};
@@ -2928,7 +2964,7 @@ struct DeviceCtx : Evaluator {
     log->theta10.assign(std::min<size_t>(log->sweeps / 10, (size_t)theta_cap), 0.0);
     if (!log->theta10.empty())
       HIP_OK(hipMemcpy(log->theta10.data(), d_th, log->theta10.size() * sizeof(double), hipMemcpyDeviceToHost));
-    for (void* pf : {(void*)d_a, (void*)d_v, (void*)d_g, (void*)d_sw, (void*)d_bar, (void*)d_th}) (void)hipFree(pf);
+    for (void* pf : {(void*)d_a, (void*)d_v, (void*)d_g, (void*)d_sw, (void*)d_th}) (void)hipFree(pf);
     return true;
   }
 
@@ -2943,30 +2979,62 @@ struct DeviceCtx : Evaluator {
     }
     resident_mu(mu);  // X is centred in place: Y = W·X
     ystore_upload(w, nc, nf);
-    const bool mfma_path = nc <= 64;  // larger nc: the VALU tile kernel
+    const bool mfma_path = nc <= 64;  // larger nc: the VALU tile kernel (symmetric upper tiles)
     const uint64_t CH = mfma_path ? (1ull << 22) : (1ull << 16);
-    // tiles of the upper triangle and the T split (≈ whole rounds of one workgroup per CU)
     const int nt = (np + 127) / 128;
+    // (R, C) pair orders and the staircase tiles of k_moments4_mfma
+    std::vector<int> ri(np), rj(np), ci(np), cj(np);
+    {
+      int q = 0;
+      for (int b = 0; b < (int)nc; ++b)
+        for (int a = 0; a <= b; ++a) { ri[q] = a; rj[q] = b; ++q; }
+      q = 0;
+      for (int c = 0; c < (int)nc; ++c)
+        for (int d = c; d < (int)nc; ++d) { ci[q] = c; cj[q] = d; ++q; }
+    }
     std::vector<int> tpv, tqv;
-    for (int a = 0; a < nt; ++a)
-      for (int b = a; b < nt; ++b) { tpv.push_back(a); tqv.push_back(b); }
+    std::vector<unsigned char> tmask((size_t)nt * nt, 0);
+    for (int a = 0; a < nt; ++a) {
+      int bmin = INT_MAX;
+      for (int r = a * 128; r < std::min(np, a * 128 + 128); ++r) bmin = std::min(bmin, rj[r]);
+      for (int b = 0; b < nt; ++b) {
+        int cmax = -1;
+        for (int c = b * 128; c < std::min(np, b * 128 + 128); ++c) cmax = std::max(cmax, ci[c]);
+        if (bmin <= cmax) { tpv.push_back(a); tqv.push_back(b); tmask[(size_t)a * nt + b] = 1; }
+      }
+    }
     const int ntile = (int)tpv.size();
+    // ≈ three whole rounds of one workgroup per CU
     const int nsplit = mfma_path ? std::max(1, (int)std::lround(3.0 * n_cu / ntile)) : 1;
     const size_t slab_stride = (size_t)np * np;
-    const size_t need = nc * CH + (size_t)np * np + 2 * (size_t)np + 2 * (size_t)ntile +
-                        (mfma_path ? nsplit * slab_stride : 0);
+    auto dsz = [](size_t bytes) { return (bytes + sizeof(double) - 1) / sizeof(double); };
+    const size_t ints = dsz((6 * (size_t)np + 2 * (size_t)ntile) * sizeof(int) + (size_t)nt * nt);
+    const size_t need = nc * CH + (mfma_path ? 2 : 1) * (size_t)np * np + ints + (mfma_path ? nsplit * slab_stride : 0);
     double* Y = ensure(d_chunk, cap_chunk, need);
     double* acc = Y + nc * CH;
-    int* dpi = reinterpret_cast<int*>(acc + (size_t)np * np);
+    double* full = mfma_path ? acc + (size_t)np * np : acc;  // the lexicographic M (fill target)
+    int* dpi = reinterpret_cast<int*>(full + (size_t)np * np);
     int* dpj = dpi + np;
-    int* dtp = dpj + np;
+    int* dri = dpj + np;
+    int* drj = dri + np;
+    int* dci = drj + np;
+    int* dcj = dci + np;
+    int* dtp = dcj + np;
     int* dtq = dtp + ntile;
-    double* slabs = acc + (size_t)np * np + 2 * (size_t)np + 2 * (size_t)ntile;  // int arrays sized in doubles
+    unsigned char* dtm = reinterpret_cast<unsigned char*>(dtq + ntile);
+    double* slabs = full + (size_t)np * np + ints;
     HIP_OK(hipMemcpyAsync(dpi, pi.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dpj, pj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dri, ri.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(drj, rj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dci, ci.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dcj, cj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dtp, tpv.data(), ntile * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dtq, tqv.data(), ntile * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dtm, tmask.data(), tmask.size(), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemsetAsync(acc, 0, (size_t)np * np * sizeof(double), stream));
+    // the host image vectors must outlive the async copies
+    HIP_OK(hipStreamSynchronize(stream));
     const int tiles = (np + 31) / 32;
     bool first = true;
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
@@ -2975,12 +3043,17 @@ struct DeviceCtx : Evaluator {
       if (mfma_path) {
         const uint64_t nsb = (cn + 15) / 16;
         const uint64_t spb = (nsb + nsplit - 1) / nsplit;
-        const size_t lds = (size_t)(64 * 16 + 2 * 8 * 4 * 64) * sizeof(double);
-        k_moments4_mfma<<<dim3(ntile, nsplit), FUSED_THREADS, lds, stream>>>(Y, CH, cn, (int)nc, dpi, dpj, np, dtp, dtq,
-                                                                            spb, slabs, slab_stride);
+        const size_t lds = (size_t)(2 * 64 * 16 + 2 * 2 * 8 * 4 * 64) * sizeof(double);
+        static bool attr = false;
+        if (!attr) {
+          HIP_OK(hipFuncSetAttribute((const void*)k_moments4_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+          attr = true;
+        }
+        k_moments4_mfma<<<(unsigned)(ntile * nsplit), FUSED_THREADS, lds, stream>>>(
+            Y, CH, cn, (int)nc, dri, drj, dci, dcj, np, dtp, dtq, nsplit, spb, slabs, slab_stride);
         HIP_OK(hipGetLastError());
         k_moments4_reduce<<<(unsigned)(((size_t)np * np + 255) / 256), 256, 0, stream>>>(slabs, nsplit, slab_stride, np,
-                                                                                         first ? 0 : 1, acc);
+                                                                                         dtm, first ? 0 : 1, acc);
       } else {
         k_moments4<<<tiles * tiles, 256, 0, stream>>>(Y, CH, cn, (int)nc, dpi, dpj, np, acc);
       }
@@ -2988,10 +3061,15 @@ struct DeviceCtx : Evaluator {
       first = false;
     }
     allreduce(acc, (size_t)np * np);
-    HIP_OK(hipMemcpyAsync(out, acc, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, stream));
+    if (mfma_path) {
+      k_moments4_fill<<<(unsigned)(((size_t)np * np + 255) / 256), 256, 0, stream>>>(acc, dpi, dpj, (int)nc, np, full);
+      HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipMemcpyAsync(out, full, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
-    for (int p = 0; p < np; ++p)  // mirror the upper tiles
-      for (int q = 0; q < p; ++q) out[(size_t)p * np + q] = out[(size_t)q * np + p];
+    if (!mfma_path)
+      for (int p = 0; p < np; ++p)  // mirror the upper tiles
+        for (int q = 0; q < p; ++q) out[(size_t)p * np + q] = out[(size_t)q * np + p];
   }
 
 };

@@ -684,7 +684,9 @@ Mat Solver::ica_par(const Mat& w_init) {
 // pass (jade.rs:78-131) and the Jacobi sweeps on rotated copies VᵀMV kept
 // up to date per Givens rotation (same angles as jade.rs:137-185).
 Mat Solver::jade(size_t max_iter, double tol) {
-  static const int where = std::getenv("PICARD_DEVICE_JADE") ? JADE_SWEEPS_AUTO_DEVICE : JADE_SWEEPS_AUTO;
+  // the device sweeps (one cooperative launch) unless PICARD_HOST_JADE asks for the
+  // host's; either falls back to the host when the device cannot hold the matrices
+  const int where = std::getenv("PICARD_HOST_JADE") ? JADE_SWEEPS_AUTO : JADE_SWEEPS_AUTO_DEVICE;
   JadeInfo info;
   Mat w = jade_warm_start(ev_, has_k_ ? K_ : Mat::eye(nf_), nc_, has_mu_ ? mu_.data() : nullptr, (double)T_,
                           max_iter, tol, cfg_.verbose, where, &info);
@@ -725,9 +727,13 @@ Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, 
   const size_t npos = n * (n + 1) / 2;
   std::vector<double> A(npos * np);
   {
-    size_t m = 0;
+    std::vector<std::pair<size_t, size_t>> mpairs;
     for (size_t i = 0; i < n; ++i)
-      for (size_t j = i; j < n; ++j, ++m) {
+      for (size_t j = i; j < n; ++j) mpairs.emplace_back(i, j);
+#pragma omp parallel for schedule(static)
+    for (size_t m = 0; m < np; ++m) {
+      {
+        const size_t i = mpairs[m].first, j = mpairs[m].second;
         const size_t pij = pidx[i * n + j];
         auto q = [&](size_t k, size_t l) {
           const double e = m4[pij * np + pidx[k * n + l]] / t;
@@ -739,6 +745,7 @@ Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, 
         for (size_t k = 0; k < n; ++k)
           for (size_t l = k; l < n; ++l) A[pos(k, l) * np + m] = (q(k, l) + q(l, k)) / 2.0;
       }
+    }
   }
   if (verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
   Mat v = Mat::eye(n);

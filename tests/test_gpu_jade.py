@@ -77,9 +77,10 @@ def test_jade_device_sweeps_match_host_n64(c5_small, monkeypatch, pairs):
         assert np.max(np.abs(w @ w.T - np.eye(N))) <= 1e-12
 
 
-def test_jade_barrier_counter_wrap(c5_small, monkeypatch):
-    """The grid barrier's arrival counter preset just below 2^32: its targets wrap
-    during the run; the sweeps must be unchanged (bit-identical)."""
+def test_jade_sequence_base_independent(c5_small, monkeypatch):
+    """The device sweeps' granule sequence numbers started just below 2^32 (they are
+    64-bit; PICARD_JADE_BAR_BASE presets the base): the sweeps must be unchanged
+    (bit-identical) — the tags only gate, never feed, the arithmetic."""
     ctx, k, mu, _, _ = c5_small
     w0 = ctx.jade(k, mu, max_iter=2, where="device")[0]
     monkeypatch.setenv("PICARD_JADE_BAR_BASE", str(2 ** 32 - 5000))
@@ -87,14 +88,18 @@ def test_jade_barrier_counter_wrap(c5_small, monkeypatch):
     assert np.array_equal(w0, w1)
 
 
-def test_jade_verbose_lines_device(pa, c1_data, capfd, monkeypatch):
-    """jade.rs:57-66: the 'JADE iteration N: max angle' line every 10 sweeps, also
-    from the device sweeps (PICARD_DEVICE_JADE)."""
+@pytest.mark.parametrize("host", [False, True])
+def test_jade_verbose_lines(pa, c1_data, capfd, monkeypatch, host):
+    """jade.rs:57-66: the 'JADE iteration N: max angle' line every 10 sweeps, from the
+    device sweeps (default) and the host sweeps (PICARD_HOST_JADE)."""
     x, s, a = c1_data
-    monkeypatch.setenv("PICARD_DEVICE_JADE", "1")
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    if host:
+        monkeypatch.setenv("PICARD_HOST_JADE", "1")
     pa.Picard.fit_with_config(x, pa.PicardConfig(jade_it=20, max_iter=1, w_init=np.eye(8), verbose=True))
-    out = capfd.readouterr().out
-    assert "JADE iteration 10: max angle = " in out and "JADE iteration 20: max angle = " in out
+    cap = capfd.readouterr()
+    assert "JADE iteration 10: max angle = " in cap.out and "JADE iteration 20: max angle = " in cap.out
+    assert ("host sweeps" if host else "device sweeps") in cap.err
 
 
 @pytest.mark.timeout(300)

@@ -260,15 +260,20 @@ def test_fit_variants_vs_oracle(pa, po, c1_data, kw):
 
 
 @pytest.mark.parametrize("jade_it", [1, 3])
-def test_jade_device_sweeps_match_host(pa, c1_data, monkeypatch, jade_it):
-    """The Jacobi sweeps as one cooperative device launch (PICARD_DEVICE_JADE=1,
-    DeviceCtx::jade_sweeps) against the host sweeps on the same cumulant matrices: the
-    angles differ only by summation order, so after a few sweeps they agree to ~1e-12."""
+def test_jade_device_sweeps_match_host(pa, c1_data, monkeypatch, capfd, jade_it):
+    """The Jacobi sweeps as one cooperative device launch (the default,
+    DeviceCtx::jade_sweeps) against the host sweeps (PICARD_HOST_JADE=1) on the same
+    cumulant matrices: the angles differ only by summation order, so after a few sweeps
+    they agree to ~1e-12. PICARD_TRACE names the sweeps that actually ran."""
     x, s, a = c1_data
     cfg = dict(jade_it=jade_it, max_iter=1, w_init=np.eye(8))
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    monkeypatch.setenv("PICARD_HOST_JADE", "1")
     host = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg)).full_unmixing()
-    monkeypatch.setenv("PICARD_DEVICE_JADE", "1")
+    assert "host sweeps" in capfd.readouterr().err
+    monkeypatch.delenv("PICARD_HOST_JADE")
     dev = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg)).full_unmixing()
+    assert "device sweeps" in capfd.readouterr().err
     assert np.max(np.abs(dev - host)) <= 1e-9 * np.max(np.abs(host))
 
 
