@@ -466,16 +466,7 @@ __host__ __device__ inline double finalize_row(int dens, double alpha, double n,
 }
 
 // density interleave widths (register budget: fused 256 VGPRs, split kernels 128)
-#ifndef PC_FUSED_NW
-#define PC_FUSED_NW 2
-#endif
-#ifndef PC_LOSS_NW
-#define PC_LOSS_NW 1
-#endif
-#ifndef PC_FROMY_NW
-#define PC_FROMY_NW 1
-#endif
-constexpr int FUSED_NW = PC_FUSED_NW, LOSS_NW = PC_LOSS_NW, FROMY_NW = PC_FROMY_NW;
+constexpr int FUSED_NW = 2, LOSS_NW = 1, FROMY_NW = 1;
 
 // ---------------------------------------------------------------------------
 // The fused pass. NB = 16-row blocks of Y (nc ≤ 16·NB), 8 waves.
@@ -1969,7 +1960,7 @@ __global__ void k_moments4_fill(const double* __restrict__ acc, const int* __res
 // Synthetic mixture (benches/benchmarks.rs:8-35), generated in HBM.
 // S[i][t] from LCG state number i·T + t + 1 (jump-ahead per column, then the
 // fixed affine map of T steps per row), Laplace by inverse CDF; u == 0 is
-// replaced by 2^-32 (see oracle/datagen.py).
+// replaced by 2^-32.
 // ---------------------------------------------------------------------------
 struct Affine { uint64_t a, c; };
 __host__ __device__ inline Affine lcg_jump(uint64_t n) {
@@ -2290,13 +2281,8 @@ struct DeviceCtx : Evaluator {
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
     (void)nfp;
-    // NB = 8 without H: the warp-specialised 16-wave kernel (same sums);
-    // PICARD_FUSED_WS=0 selects the 8-wave k_eval_fused<8> (A/B timing)
-    static const bool ws_on = [] {
-      const char* e = std::getenv("PICARD_FUSED_WS");
-      return !(e && e[0] == '0');
-    }();
-    const bool ws = NB == 8 && !H && ws_on;
+    // NB = 8 without H: the warp-specialised 16-wave kernel (same sums as k_eval_fused<8>)
+    const bool ws = NB == 8 && !H;
     auto kern = ws ? k_eval_fused_ws<D, Q> : k_eval_fused<NB, H, D, Q>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -2638,7 +2624,6 @@ struct DeviceCtx : Evaluator {
     const int tb = 16 * (8 / nb);
     const uint64_t nblk = (n_local_ + tb - 1) / tb;
     const size_t need = (size_t)nblk * 16 * nb * tb;
-    if (std::getenv("PICARD_NO_YSTORE")) return false;  // experiment knob: never keep Y
     if (need <= cap_ybuf) return true;
     if (ybuf_failed) return false;
     size_t fr = 0, tot = 0;
@@ -2663,12 +2648,7 @@ struct DeviceCtx : Evaluator {
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * S::NCP);
     const size_t lds = (size_t)2 * S::TS * 16 * NB * 16 * sizeof(double);
     // NB = 8 on the centred resident X: LDS-DMA staging, two blocks per barrier
-    // (PICARD_LOSS2=0 selects k_eval_loss<8>, for A/B timing)
-    static const bool loss2_on = [] {
-      const char* e = std::getenv("PICARD_LOSS2");
-      return !(e && e[0] == '0');
-    }();
-    if (NB == 8 && dmu == nullptr && loss2_on) {
+    if (NB == 8 && dmu == nullptr) {
       const size_t lds2 = (size_t)2 * 2 * 128 * 16 * sizeof(double);
       HIP_OK(hipEventRecord(ev[1], stream));
       if (store)

@@ -147,6 +147,20 @@ def test_multi_try_schedule_matches_per_try(pa, rng, monkeypatch):
     assert np.max(np.abs(r1.unmixing - r2.unmixing)) <= 1e-6
 
 
+@pytest.mark.parametrize("knob", ["PICARD_KEEP_Y", "PICARD_SPLIT_FIRST"])
+def test_ortho_schedule_knobs_bit_identical(pa, rng, monkeypatch, knob):
+    """The orthogonal line-search schedules (host_solver.hpp: Y kept in HBM for the
+    completion; try 1 loss-only) change which passes run, never the sums: the fit is
+    bit-identical to the default schedule (64 < N ≤ 128: the split kernels)."""
+    x = laplace_mix(rng, 96, 20000)
+    cfg = dict(max_iter=40, random_state=5)
+    r1 = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg))
+    monkeypatch.setenv(knob, "1")
+    r2 = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg))
+    assert r1.n_iterations == r2.n_iterations and r1.converged == r2.converged
+    assert np.array_equal(r1.unmixing, r2.unmixing)
+
+
 def test_eval_deterministic(pa, rng):
     x = laplace_mix(rng, 64, 20000)
     ctx = ctx_with(pa, x)
