@@ -257,14 +257,14 @@ void Solver::complete(EvalStats* out) {
 }
 
 // core.rs:39-85 + loss_to_f64 core.rs:90-96, from the pass's per-row sums
-double Solver::loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular) {
+double Solver::loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular,
+                       double sg, double la) {
   const double t = (double)T_;
   const bool ortho = cfg_.ortho != 0;
   double loss = 0.0;
   *singular = false;
   if (!ortho) {
-    double sg, la;
-    sln_det(w, &sg, &la);
+    if (std::isnan(sg)) sln_det(w, &sg, &la);  // not given by the caller
     if (sg == 0.0) { *singular = true; return 1e15; }
     loss = -la;
   }
@@ -431,18 +431,29 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         ls.nc = n;
         ls.has_h = false;
         ls.buf.assign(EvalStats::size(n, false), 0.0);
+        // every try's W_j = (I + α_j D)·W and log|det W_j| (core.rs:124-125, :43-47),
+        // formed for all tries at once on the host threads; each is the same serial
+        // arithmetic as in the walk below, which then accepts in the reference order
+        std::vector<Mat> wj(na);
+        std::vector<double> dsg(na), dla(na);
+        wj[0] = r.w;
+#pragma omp parallel for schedule(dynamic, 1) if (na > 1)
+        for (size_t j = 0; j < na; ++j) {
+          if (j > 0) {
+            Mat tj = Mat::eye(n);
+            for (size_t e = 0; e < tj.a.size(); ++e) tj.a[e] += alphas[j] * direction.a[e];
+            wj[j] = matmul(tj, W_);
+          }
+          sln_det(wj[j], &dsg[j], &dla[j]);
+        }
         for (size_t j = 0; j < na; ++j) {
           const double a = alphas[j];
-          if (j > 0) {
-            transform = Mat::eye(n);
-            for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += a * direction.a[e];
-            r.w = matmul(transform, W_);
-          }
+          r.w = std::move(wj[j]);
           std::memcpy(const_cast<double*>(ls.ll()), ll.data() + j * n, n * sizeof(double));
           std::memcpy(const_cast<double*>(ls.y2()), y2.data() + j * n, n * sizeof(double));
           r.tries = k + j + 1;
           bool singular;
-          const double loss = loss_of(ls, r.w, signs_, &singular);
+          const double loss = loss_of(ls, r.w, signs_, &singular, dsg[j], dla[j]);
           if (loss < current_loss_) {
             evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
             r.partial = false;

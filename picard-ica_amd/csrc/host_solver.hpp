@@ -2,6 +2,7 @@
 // src/lbfgs.rs:84-171 + src/jade.rs:22-197 restated over an Evaluator.
 #pragma once
 #include <deque>
+#include <limits>
 #include <memory>
 #include <random>
 
@@ -53,7 +54,9 @@ class Solver {
 
  private:
   std::unique_ptr<TransformWorker> ahead_;
-  double loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular);
+  // sg / la: sign and log|det w| when the caller already has them (NaN: computed here)
+  double loss_of(const EvalStats& s, const Mat& w, const std::vector<double>& signs, bool* singular,
+                 double sg = std::numeric_limits<double>::quiet_NaN(), double la = 0.0);
   void evaluate(const Mat& w_core, EvalStats* out);
   bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
   void complete(EvalStats* out);
