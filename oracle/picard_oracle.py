@@ -24,8 +24,10 @@ Parity pinning:
     ndarray 0.17.1/cblas-sys 0.1.4; LAPACK eigh/svd/getrf via
     ndarray-linalg 0.18.0 / lax 0.18.0) is restated with numpy's bundled
     OpenBLAS/LAPACK (numpy 2.2), which implements the same LAPACK routines.
-  * rand 0.9.2 StdRng (ChaCha12) + rand_distr 0.5.1 StandardNormal is not
-    reproducible offline; runs that need bit-parity pass an explicit w_init.
+  * rand 0.9.2 StdRng (ChaCha12) + rand_distr 0.5.1 StandardNormal (the seeded
+    random w_init) are restated in ``oracle/rust_rand.py`` from the crates'
+    published algorithms (ChaCha pinned by RFC 8439; the composition itself is
+    parity unpinned — no reference-held vector exists offline).
 
 Every function cites the reference file:line it follows.
 """
@@ -36,6 +38,11 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
 import numpy as np
+
+try:
+    from . import rust_rand
+except ImportError:  # imported as a top-level module (tests put oracle/ on sys.path)
+    import rust_rand
 
 # ---------------------------------------------------------------------------
 # error.rs:9-42 — PicardError variants (as Python exceptions)
@@ -736,8 +743,10 @@ def fit_with_config(x: np.ndarray, config: PicardConfig, w_init_random=None) -> 
         w_init = w_init.copy()
     else:
         if w_init_random is None:
-            rng = np.random.default_rng(config.random_state)
-            w_init_random = rng.standard_normal((actual, actual))
+            if config.random_state is not None:  # solver.rs:56-58, :112-118 (oracle/rust_rand.py)
+                w_init_random = np.array(rust_rand.random_w_init(config.random_state, actual))
+            else:  # solver.rs:59: an OS-entropy stream (not reproducible by design)
+                w_init_random = np.random.default_rng().standard_normal((actual, actual))
         w_init = sym_decorrelation(np.asarray(w_init_random, dtype=np.float64))
     if config.jade_it is not None:
         w_init = jade(x1, config.jade_it, 1e-6, config.verbose)

@@ -5,6 +5,7 @@
 //   src/lbfgs.rs:84-171, src/whitening.rs:48-107, src/jade.rs:22-197
 // Every N×T quantity comes from the Evaluator (one fused device pass).
 #include "host_solver.hpp"
+#include "host_rng.hpp"
 
 #include <atomic>
 #include <chrono>
@@ -89,23 +90,6 @@ void regularize_hessian(Mat& h, const std::vector<double>& h_off, double lambda_
     }
 }
 
-// ---------------------------------------------------------- rng (w_init)
-// rand 0.9.2 StdRng/ChaCha12 + rand_distr ziggurat are not reproducible
-// offline; a seeded SplitMix64 + Box–Muller stands in. Runs
-// that need reference bit-parity pass an explicit w_init.
-namespace {
-struct SplitMix {
-  uint64_t s;
-  uint64_t next() {
-    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-  }
-  double uniform() { return ((next() >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
-};
-}  // namespace
-
 // ------------------------------------------------------------- Solver
 Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   // config.rs:104-142
@@ -126,7 +110,9 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   const uint64_t n = nf_, p = T_;
   if (n == 0 || p == 0) throw invalid_dimensions("Input matrix cannot be empty");  // solver.rs:50-54
 
-  SplitMix rng{cfg.has_random_state ? cfg.random_state : (uint64_t)std::random_device{}() << 32 ^ std::random_device{}()};
+  // solver.rs:56-60: StdRng::seed_from_u64(seed), or an unseeded (OS-entropy) stream
+  RustStdRng rng{cfg.has_random_state ? cfg.random_state
+                                      : (uint64_t)std::random_device{}() << 32 ^ std::random_device{}()};
   const uint64_t mn = n < p ? n : p;
   uint64_t ncomp = cfg.has_n_components ? cfg.n_components : mn;
   if (ncomp > mn) ncomp = mn;  // solver.rs:63
@@ -191,13 +177,8 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
     w_init_ = Mat(nc_, nc_);
     w_init_.a = w_init_user_;
   } else {
-    Mat w(nc_, nc_);
-    for (size_t i = 0; i < nc_ * nc_; i += 2) {
-      const double u1 = rng.uniform(), u2 = rng.uniform();
-      const double r = std::sqrt(-2.0 * std::log(u1));
-      w.a[i] = r * std::cos(2.0 * M_PI * u2);
-      if (i + 1 < nc_ * nc_) w.a[i + 1] = r * std::sin(2.0 * M_PI * u2);
-    }
+    Mat w(nc_, nc_);  // solver.rs:112-118: StandardNormal draws, row-major
+    for (size_t i = 0; i < nc_ * nc_; ++i) w.a[i] = rng.standard_normal();
     if (!sym_decorrelation(w, &w_init_)) throw singular_matrix();
   }
   // warm starts: solver.rs:124-137
