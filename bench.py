@@ -5,7 +5,9 @@ Workload (BASELINE.json configs[2] — the config the metric is quoted on; at
 102.4 GB it fits one MI355X's 288 GB, so N=1 runs it whole): 128 sources ×
 1e8 samples of the reference bench mixture (benches/benchmarks.rs:8-35, seed
 42), generated directly in HBM, Picard-O (ortho=True, extended defaults to
-ortho), tanh, tol=1e-7, max_iter=500, m=7, ls_tries=10, whitening + centering.
+ortho), tanh, tol=1e-7, max_iter=500, m=7, ls_tries=10, whitening + centering,
+random_state(42) as the reference's benches set it (benchmarks.rs:69,95,119): the
+random w_init is the reference's own StdRng/StandardNormal stream (host_rng.cpp).
 
 A "step" is ONE Picard-O iteration (src/core.rs:211-391): every fused pass
 of its line search, the RCCL all-reduce (N>1), the D2H copy and the host N×N
@@ -71,7 +73,7 @@ def run_config(pa, name, seed):
     ctx = pa.DeviceContext(0)
     a = ctx.generate(n, t, seed)
     t0 = time.perf_counter()
-    sv = pa.Solver(ctx, pa.PicardConfig(random_state=0, want_sources=False, **c["kw"]))
+    sv = pa.Solver(ctx, pa.PicardConfig(random_state=42, want_sources=False, **c["kw"]))
     t_setup = time.perf_counter() - t0
     ctx.kernel_breakdown(reset=True)
     t1 = time.perf_counter()
@@ -168,7 +170,7 @@ def main():
     pa.device_synchronize(local_rank)
     t_gen = time.perf_counter() - t_gen
 
-    cfg = pa.PicardConfig(ortho=True, max_iter=500, tol=1e-7, random_state=0, want_sources=False)
+    cfg = pa.PicardConfig(ortho=True, max_iter=500, tol=1e-7, random_state=42, want_sources=False)
     t_setup = time.perf_counter()
     solver = pa.Solver(ctx, cfg)   # centering, whitening Gram, w_init, initial pass
     t_setup = time.perf_counter() - t_setup

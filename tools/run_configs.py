@@ -27,7 +27,7 @@ def run(name, oracle=False, max_iter=None):
     ctx = pa.DeviceContext(0)
     a = ctx.generate(n, t, 42)
     t0 = time.perf_counter()
-    s = pa.Solver(ctx, pa.PicardConfig(random_state=0, want_sources=False, **kw))
+    s = pa.Solver(ctx, pa.PicardConfig(random_state=42, want_sources=False, **kw))
     t_setup = time.perf_counter() - t0
     ctx.kernel_breakdown(reset=True)
     t1 = time.perf_counter()
@@ -46,7 +46,7 @@ def run(name, oracle=False, max_iter=None):
         from oracle import picard_oracle as po
         x = ctx.download()
         t2 = time.perf_counter()
-        ro = po.fit_with_config(x, po.PicardConfig(random_state=0, **c["kw"]),
+        ro = po.fit_with_config(x, po.PicardConfig(random_state=42, **c["kw"]),
                                 w_init_random=None)
         out["oracle_s"] = time.perf_counter() - t2
         out["oracle_amari"] = po.amari_distance(ro.full_unmixing(), a)
