@@ -266,6 +266,20 @@ void pc_ctx_kernel_stats(pc_ctx* ctx, double* kernel_ms, double* call_ms, uint64
 /* Per kernel kind since the last reset: [0] fused pass, [1] loss-only try,
  * [2] completion from kept Y — summed HIP-event kernel ms and launch counts. */
 void pc_ctx_kernel_breakdown(pc_ctx* ctx, double ms[4], uint64_t n[4], int32_t reset);
+/* Y-stage arithmetic of the passes (Y = W·(X−μ), core.rs:124). PC_YSTAGE_AUTO
+ * (default): where the shape allows (64 < nc ≤ 128, n_features ≤ 128) the
+ * loss-only line-search pass forms Y on the i8 matrix cores from exact int8
+ * digits of X (7 radix-256 digits per value, one exponent per sample, built
+ * once per resident mean) and of W (7 per value, one exponent per row): every
+ * digit product is summed exactly in int32 and the 7 leading diagonals are
+ * combined in fp64, so Y carries the accuracy of an fp64 GEMM (DESIGN.md §3,
+ * the Ozaki scheme); the digit image costs another 7 bytes per element of HBM. PC_YSTAGE_F64: every pass on the
+ * fp64 MFMA Y stage. Either way the statistics agree with the fp64 oracle to
+ * 1e-12 relative; they are bit-identical only within one mode. */
+enum { PC_YSTAGE_AUTO = 0, PC_YSTAGE_F64 = 1 };
+int pc_ctx_set_y_stage(pc_ctx* ctx, int32_t mode);
+/* number of passes whose Y stage ran on the int8 slices since the context was created */
+uint64_t pc_ctx_int8_passes(const pc_ctx* ctx);
 /* hipDeviceSynchronize on `device` (bench bracketing). */
 int pc_device_synchronize(int32_t device);
 

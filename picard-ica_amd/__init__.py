@@ -174,6 +174,8 @@ def _load():
         "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
         "pc_device_synchronize": (C.c_int, [i32]),
         "pc_ctx_kernel_breakdown": (None, [vp, d, P(u64), i32]),
+        "pc_ctx_set_y_stage": (C.c_int, [vp, i32]),
+        "pc_ctx_int8_passes": (u64, [vp]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -197,7 +199,7 @@ EXPORTED = [
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 
@@ -601,6 +603,15 @@ class DeviceContext:
         n = (C.c_uint64 * 4)()
         lib.pc_ctx_kernel_breakdown(self.h, ms, n, int(reset))
         return {k: (ms[i], n[i]) for i, k in enumerate(("fused", "loss", "fromy", "multi"))}
+
+    def set_y_stage(self, mode: str = "auto"):
+        """pc_ctx_set_y_stage: "auto" (int8-slice Y stage where the shape allows) or "f64"."""
+        _raise(lib.pc_ctx_set_y_stage(self.h, {"auto": 0, "f64": 1}[mode]), _errbuf())
+
+    @property
+    def int8_passes(self) -> int:
+        """pc_ctx_int8_passes: passes whose Y stage ran on the int8 slices so far."""
+        return int(lib.pc_ctx_int8_passes(self.h))
 
     def rowsum(self) -> np.ndarray:
         out = np.empty(self.n_features)

@@ -27,6 +27,8 @@ int rccl_unique_id(char* out);
 void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, uint64_t* n, int reset);
 void device_synchronize(int device);
 void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset);
+void device_ctx_set_y_stage(Evaluator* e, int mode);
+uint64_t device_ctx_int8_passes(const Evaluator* e);
 }  // namespace pcamd
 
 using namespace pcamd;
@@ -390,6 +392,14 @@ void pc_ctx_kernel_stats(pc_ctx* c, double* kernel_ms, double* call_ms, uint64_t
 void pc_ctx_kernel_breakdown(pc_ctx* c, double ms[4], uint64_t n[4], int32_t reset) {
   device_ctx_kernel_breakdown(c->ev.get(), ms, n, reset);
 }
+
+int pc_ctx_set_y_stage(pc_ctx* c, int32_t mode) {
+  if (mode != PC_YSTAGE_AUTO && mode != PC_YSTAGE_F64) return PC_ERR_INVALID_CONFIG;
+  device_ctx_set_y_stage(c->ev.get(), mode);
+  return PC_OK;
+}
+
+uint64_t pc_ctx_int8_passes(const pc_ctx* c) { return device_ctx_int8_passes(c->ev.get()); }
 
 int pc_device_synchronize(int32_t device) {
   try {

@@ -380,7 +380,7 @@ __device__ __forceinline__ void density_acc4(const d4& y, double alpha, double m
 }
 
 // ℓ terms only (line-search tries): identical arithmetic to density_acc4's ℓ part
-template <int DENS, bool NEED_Q, int NW = 4>
+template <int DENS, bool NEED_Q, int NW = 4, bool SCHED_FENCE = true>
 __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a, const double* tab, RowAcc& a) {
   if constexpr (NEED_Q || DENS == DENS_CUBE)  // as density_acc4 (cube's fused pass keeps Σy²)
 #pragma unroll
@@ -398,7 +398,7 @@ __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a,
         a.l += fabs(y[g + i]);
         a.p *= 2.0 + em;
       }
-      __builtin_amdgcn_sched_barrier(0);  // one group's chain live at a time
+      if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // one group's chain live at a time
     } else if constexpr (DENS == DENS_EXP) {
       double x[NW], emr[NW], sc[NW];
 #pragma unroll
@@ -877,6 +877,7 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
 }
 
 #include "loss2.inc"
+#include "ozaki.inc"
 
 template <int NB, bool NEED_H, int DENS>
 __global__ void __launch_bounds__(FUSED_THREADS, 4)
@@ -2039,6 +2040,8 @@ struct DeviceCtx : Evaluator {
     if (comm) ncclCommDestroy(comm);
     for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src})
       if (p) (void)hipFree(p);
+    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsl, (void*)d_wsc})
+      if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -2051,7 +2054,13 @@ struct DeviceCtx : Evaluator {
   double* ensure(double*& p, size_t& cap, size_t n) {
     if (n > cap) {
       if (p) HIP_OK(hipFree(p));
-      HIP_OK(hipMalloc(&p, n * sizeof(double)));
+      p = nullptr;
+      cap = 0;
+      if (hipMalloc(&p, n * sizeof(double)) != hipSuccess) {
+        (void)hipGetLastError();
+        release_xsl();  // the int8 slice image is a cache: its HBM goes to the pass buffers
+        HIP_OK(hipMalloc(&p, n * sizeof(double)));
+      }
       cap = n;
     }
     return p;
@@ -2063,6 +2072,8 @@ struct DeviceCtx : Evaluator {
     nf = nf_; n_local_ = n_local; n_total = n_tot; t0 = t0_;
     xshift_.clear();
     raw_sums_.clear();
+    release_xsl();  // a new X: its slice image is rebuilt on demand
+    xsl_failed_ = false;
     ldx = (n_local + 127) / 128 * 128;  // a fused-pass tile (≤ 128 samples) never crosses a row end
     if (ldx == 0) ldx = 128;
     HIP_OK(hipMalloc(&X, nf * ldx * sizeof(double) + 256));
@@ -2213,6 +2224,7 @@ struct DeviceCtx : Evaluator {
   double* d_shift_part = nullptr; size_t cap_shift_part = 0;
   void shift_rows(const double* mu_host, bool undo) {
     if (!n_local_) return;
+    drop_xsl();  // the slice image follows the resident X
     double* dmu = ensure(d_mu, cap_mu, nf);
     HIP_OK(hipMemcpyAsync(dmu, mu_host, nf * sizeof(double), hipMemcpyHostToDevice, stream));
     const unsigned gx = (unsigned)std::min<uint64_t>((n_local_ / 2 + 255) / 256 + 1, std::max(1, 4 * n_cu));
@@ -2639,10 +2651,119 @@ struct DeviceCtx : Evaluator {
     return true;
   }
 
+  // ---- int8-slice Y stage (ozaki.inc) ---------------------------------------
+  // The slice image of the centred resident X is built once per resident μ
+  // (k_slice_x) and dropped whenever X changes (alloc_x, shift_rows). y_stage_
+  // = PC_YSTAGE_F64 keeps every pass on the fp64 MFMA Y stage.
+  uint8_t* d_xsl = nullptr;
+  double* d_xsc = nullptr;
+  size_t cap_xsl = 0;
+  bool xsl_valid_ = false, xsl_failed_ = false;
+  uint8_t* d_wsl = nullptr;
+  double* d_wsc = nullptr;
+  int y_stage_ = 0;
+  uint64_t n_int8_passes_ = 0;
+  bool d_wsl_ready_ = false;
+  void drop_xsl() { xsl_valid_ = false; }
+  // free the slice image for good (until the next load / generate): the fp64 Y stage
+  // serves every pass from then on
+  void release_xsl() {
+    if (d_xsl) { HIP_OK(hipStreamSynchronize(stream)); (void)hipFree(d_xsl); (void)hipFree(d_xsc); }
+    d_xsl = nullptr; d_xsc = nullptr; cap_xsl = 0;
+    xsl_valid_ = false;
+    xsl_failed_ = true;
+  }
+  // the shapes the i8 loss kernel covers: 64 < nc ≤ 128, nf ≤ 128, centred X
+  bool oz_shape(size_t nc) const { return y_stage_ == 0 && pick_nb(nc) == 8 && nf <= 128 && nf > 0; }
+  bool ensure_xsl() {
+    if (xsl_valid_) return true;
+    if (xsl_failed_) return false;
+    const uint64_t n_blocks = ldx / 16;
+    const size_t need = (size_t)n_blocks * OZ_BLOCK_BYTES;
+    if (need > cap_xsl) {
+      size_t fr = 0, tot = 0;
+      HIP_OK(hipMemGetInfo(&fr, &tot));
+      if (d_xsl) { HIP_OK(hipFree(d_xsl)); HIP_OK(hipFree(d_xsc)); fr += cap_xsl + ldx * sizeof(double); }
+      d_xsl = nullptr; d_xsc = nullptr; cap_xsl = 0;
+      // keep ≥ 4 GB free next to X for the pass buffers; otherwise stay on fp64
+      if (need + ldx * sizeof(double) + (size_t(4) << 30) > fr || hipMalloc(&d_xsl, need) != hipSuccess ||
+          hipMalloc(&d_xsc, ldx * sizeof(double)) != hipSuccess) {
+        (void)hipGetLastError();
+        if (d_xsl) (void)hipFree(d_xsl);
+        d_xsl = nullptr; d_xsc = nullptr;
+        xsl_failed_ = true;
+        return false;
+      }
+      cap_xsl = need;
+    }
+    const unsigned grid = (unsigned)std::min<uint64_t>(n_blocks, (uint64_t)n_cu * 16);
+    k_slice_x<<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
+    HIP_OK(hipGetLastError());
+    xsl_valid_ = true;
+    return true;
+  }
+  // W (nc × nf, host) → slice image [wave][a][kstep][lane][16 B] + row scales 2^(f_i − 12)
+  void upload_wsl(const double* w, size_t nc) {
+    constexpr size_t IMG = (size_t)8 * OZ_SLICES * 2 * 64 * 16;
+    std::vector<uint8_t> img(IMG, 0);
+    std::vector<double> sc(128, 0x1p-12);
+    for (size_t i = 0; i < nc; ++i) {
+      double mx = 0.0;
+      for (size_t k = 0; k < nf; ++k) mx = std::fmax(mx, std::fabs(w[i * nf + k]));
+      int e = 0;
+      if (mx > 0.0) (void)std::frexp(mx, &e);
+      sc[i] = std::ldexp(1.0, e - 12);
+      const size_t wave = i >> 4, n = i & 15;
+      for (size_t k = 0; k < nf; ++k) {
+        int dg[OZ_SLICES];
+        oz_digits(std::ldexp(w[i * nf + k], 6 - e), dg);
+        const size_t s = k >> 6, lane = n + 16 * ((k >> 4) & 3), j = k & 15;
+        for (int a = 0; a < OZ_SLICES; ++a)
+          img[(((wave * OZ_SLICES + a) * 2 + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
+      }
+    }
+    if (!d_wsl) {
+      HIP_OK(hipMalloc(&d_wsl, IMG));
+      HIP_OK(hipMalloc(&d_wsc, 128 * sizeof(double)));
+    }
+    HIP_OK(hipMemcpyAsync(d_wsl, img.data(), IMG, hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsc, sc.data(), 128 * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));  // the host images must outlive the copies
+  }
+  template <int D, bool Q>
+  void launch_loss_oz(double alpha, bool store, double* st_rows) {
+    const uint64_t n_blocks = (n_local_ + 15) / 16;
+    uint64_t bpw;
+    const int nwg = partition(n_blocks, &bpw);
+    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * 128);
+    const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
+    auto kern = store ? k_eval_loss_oz<D, true, Q> : k_eval_loss_oz<D, false, Q>;
+    static bool attr[2] = {false, false};
+    if (!attr[store]) {
+      HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr[store] = true;
+    }
+    HIP_OK(hipEventRecord(ev[1], stream));
+    kern<<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, alpha, bpw, n_blocks, part,
+                                              store ? d_ybuf : nullptr);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
+        part, nwg, 2 * 128, 0, 128, (int)kept_nc_pending, 2, st_rows, D, alpha, (double)n_local_, 1);
+    HIP_OK(hipGetLastError());
+    ++n_int8_passes_;
+  }
+
   template <int NB, int D, bool Q>
   void launch_loss(const double* dmu, double alpha, bool store, double* st_rows) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
+    if constexpr (NB == 8) {
+      if (dmu == nullptr && oz_shape(kept_nc_pending) && d_wsl_ready_) {
+        launch_loss_oz<D, Q>(alpha, store, st_rows);
+        return;
+      }
+    }
     uint64_t bpw;
     const int nwg = partition(n_blocks, &bpw);
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * S::NCP);
@@ -2765,7 +2886,12 @@ struct DeviceCtx : Evaluator {
     ensure(d_w, cap_w, wp.size());
     HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
     kept_nc_pending = nc;
-#define PC_LOSS(NBV, Q)                                                                         \
+    d_wsl_ready_ = false;
+    if (dmu == nullptr && oz_shape(nc) && ensure_xsl()) {
+      upload_wsl(w, nc);
+      d_wsl_ready_ = true;
+    }
+#define PC_LOSS(NBV, Q)                                                                       \
   switch (d.kind) {                                                                             \
     case DENS_TANH: launch_loss<NBV, DENS_TANH, Q>(dmu, d.alpha, store, st_rows); break;         \
     case DENS_EXP: launch_loss<NBV, DENS_EXP, Q>(dmu, d.alpha, store, st_rows); break;           \
@@ -3095,6 +3221,11 @@ void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int rese
     d->n_kernel = d->n_loss = d->n_fromy = d->n_split = d->n_multi = 0;
   }
 }
+void device_ctx_set_y_stage(Evaluator* e, int mode) {
+  auto* d = static_cast<DeviceCtx*>(e);
+  d->y_stage_ = mode;
+}
+uint64_t device_ctx_int8_passes(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_int8_passes_; }
 void device_synchronize(int device) {
   HIP_OK(hipSetDevice(device));
   HIP_OK(hipDeviceSynchronize());

@@ -99,9 +99,11 @@ def test_skip_y2_changes_nothing_else(pa, rng, n, dens):
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
 @pytest.mark.parametrize("need_h,need_y2", [(False, True), (True, True), (False, False)])
 def test_split_eval_bit_identical(pa, rng, n, dens, need_h, need_y2):
-    """Loss-only try + completion from the kept Y == one fused pass, bit for bit."""
+    """Loss-only try + completion from the kept Y == one fused pass, bit for bit (fp64 Y
+    stage in both; the int8-slice stage is checked against these in test_gpu_int8.py)."""
     x = laplace_mix(rng, n, 4099)
     ctx = ctx_with(pa, x)
+    ctx.set_y_stage("f64")
     w = rng.normal(size=(n, n)) / np.sqrt(n)
     mu = x.mean(axis=1)
     d = pa.DensityType(["tanh", "exp", "cube"].index(dens[0]), dens[1])
@@ -154,9 +156,20 @@ def test_ortho_schedule_knobs_bit_identical(pa, rng, monkeypatch, knob):
     bit-identical to the default schedule (64 < N ≤ 128: the split kernels)."""
     x = laplace_mix(rng, 96, 20000)
     cfg = dict(max_iter=40, random_state=5)
-    r1 = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg))
+
+    def fit():
+        ctx = ctx_with(pa, x)
+        ctx.set_y_stage("f64")  # one Y-stage arithmetic for every pass kind
+        sv = pa.Solver(ctx, pa.PicardConfig(**cfg))
+        while not sv.step():
+            pass
+        r = sv.finish()
+        sv.close()
+        return r
+
+    r1 = fit()
     monkeypatch.setenv(knob, "1")
-    r2 = pa.Picard.fit_with_config(x, pa.PicardConfig(**cfg))
+    r2 = fit()
     assert r1.n_iterations == r2.n_iterations and r1.converged == r2.converged
     assert np.array_equal(r1.unmixing, r2.unmixing)
 

@@ -1,0 +1,40 @@
+"""Time the loss-only line-search pass alone (HIP events around the kernel), int8-slice
+and fp64 Y stages. Usage: python tools/bench_loss.py N T [reps] [mode ...]"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import picard_ica_amd as pa  # noqa: E402
+
+n = int(sys.argv[1]); t = int(float(sys.argv[2]))
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+modes = sys.argv[4:] or ["auto", "f64"]
+ctx = pa.DeviceContext(0)
+ctx.generate(n, t, 42)
+mu = ctx.rowsum() / t
+w = np.ascontiguousarray(np.linalg.qr(np.random.default_rng(0).normal(size=(n, n)))[0] * 0.05)
+d = pa.DensityType.tanh()
+st = np.empty(n * n + 3 * n)
+kept = C.c_int32()
+err = C.create_string_buffer(1024)
+for mode in modes:
+    ctx.set_y_stage(mode)
+    call = lambda: lib_call()  # noqa: E731
+
+    def lib_call():
+        rc = pa.lib.pc_ctx_eval_loss(ctx.h, w.ctypes.data_as(C.POINTER(C.c_double)), n,
+                                     mu.ctypes.data_as(C.POINTER(C.c_double)), d._c(), 2,
+                                     st.ctypes.data_as(C.POINTER(C.c_double)), C.byref(kept), err, len(err))
+        assert rc == 0, err.value
+    lib_call()
+    ctx.kernel_breakdown(reset=True)
+    for _ in range(reps):
+        lib_call()
+    ms, nl = ctx.kernel_breakdown()["loss"]
+    avg = ms / max(nl, 1)
+    fl = 2.0 * n * n * t
+    print(f"{mode:5s} N={n} T={t}: loss kernel {avg:.3f} ms  {fl / avg / 1e9:.2f} TF/s-equiv "
+          f"({fl / avg / 1e9 / 78.6 * 100:.1f}% of fp64 78.6)  int8 passes {ctx.int8_passes}", flush=True)
