@@ -750,6 +750,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 // of barriers. Same block partition, G-tile map, k order, lane map and row-term
 // formulas as k_eval_fused<8> / k_eval_loss<8> / k_eval_fromy<8>: identical sums.
 // ---------------------------------------------------------------------------
+#include "ozaki.inc"
 #include "fused_ws.inc"
 
 // ---------------------------------------------------------------------------
@@ -877,7 +878,6 @@ k_eval_loss(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf
 }
 
 #include "loss2.inc"
-#include "ozaki.inc"
 
 template <int NB, bool NEED_H, int DENS>
 __global__ void __launch_bounds__(FUSED_THREADS, 4)
@@ -2293,18 +2293,27 @@ struct DeviceCtx : Evaluator {
     double* part = ensure(d_part, cap_part, (size_t)nwg * pstride);
     const size_t lds = (size_t)(2 * S::TS * nfp * 16 + 2 * (H ? 3 : 2) * S::FRAGS) * sizeof(double);
     (void)nfp;
-    // NB = 8 without H: the warp-specialised 16-wave kernel (same sums as k_eval_fused<8>)
+    // NB = 8 without H: the warp-specialised 16-wave kernel (same sums as k_eval_fused<8>),
+    // on the int8-digit Y stage when the digit image is there (not for the Gram)
     const bool ws = NB == 8 && !H;
-    auto kern = ws ? k_eval_fused_ws<D, Q> : k_eval_fused<NB, H, D, Q>;
-    static bool attr_set = false;
-    if (!attr_set) {
-      HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
-      attr_set = true;
+    const bool oz = ws && D != DENS_LINEAR && dmu == nullptr && oz_fused_ready_;
+    auto kws = oz ? k_eval_fused_ws<D, Q, true> : k_eval_fused_ws<D, Q, false>;
+    auto kfu = k_eval_fused<NB, H, D, Q>;
+    static bool attr_set[3] = {false, false, false};
+    const int ak = ws ? (oz ? 2 : 1) : 0;
+    if (!attr_set[ak]) {
+      HIP_OK(hipFuncSetAttribute(ws ? (const void*)kws : (const void*)kfu, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 160 * 1024 - EXP_TAB_BYTES));
+      attr_set[ak] = true;
     }
     HIP_OK(hipEventRecord(ev[1], stream));
-    kern<<<nwg, ws ? WS_THREADS : FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw,
-                                                                n_blocks, part);
+    if (ws)
+      kws<<<nwg, WS_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part, d_xsl, d_xsc,
+                                           d_wsl, d_wsc);
+    else
+      kfu<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part);
     HIP_OK(hipGetLastError());
+    if (oz) ++n_int8_passes_;
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t total = EvalStats::size(nc, H);
     k_reduce<<<(total + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
@@ -2356,6 +2365,11 @@ struct DeviceCtx : Evaluator {
         for (size_t k = 0; k < nf; ++k) wp[i * nfp + k] = w[i * nf + k];
       ensure(d_w, cap_w, wp.size());
       HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+      oz_fused_ready_ = false;
+      if (dmu == nullptr && !need_h && dens != DENS_LINEAR && oz_shape(nc) && ensure_xsl()) {
+        upload_wsl(w, nc);
+        oz_fused_ready_ = true;
+      }
       switch (nb) {
         case 1: dispatch_h<1>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
         case 2: dispatch_h<2>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
@@ -2663,7 +2677,7 @@ struct DeviceCtx : Evaluator {
   double* d_wsc = nullptr;
   int y_stage_ = 0;
   uint64_t n_int8_passes_ = 0;
-  bool d_wsl_ready_ = false;
+  bool d_wsl_ready_ = false, oz_fused_ready_ = false;
   void drop_xsl() { xsl_valid_ = false; }
   // free the slice image for good (until the next load / generate): the fp64 Y stage
   // serves every pass from then on

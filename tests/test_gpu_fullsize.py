@@ -6,10 +6,9 @@ size-independent checks the domain offers:
   * orthogonal invariance: for Y = Q·K·(X − μ) with Q orthogonal,
     Σ_i Σ_t y_it² = N·T — to 1e-10 relative;
   * the split evaluation (loss-only try + completion) is bit-identical to the
-    fused pass on the fp64 Y stage, and the skipped-Σy² pass changes no other
-    statistic;
-  * the loss-only try on the int8-digit Y stage (the default at this shape) agrees
-    with the fp64 fused pass to 1e-13 relative and keeps Σ y² = N·T to 1e-10.
+    fused pass on either Y stage (int8 digits, the default here, and fp64), and
+    the skipped-Σy² pass changes no other statistic;
+  * the two Y stages agree to 1e-13 relative and both keep Σ y² = N·T to 1e-10.
 """
 import numpy as np
 import pytest
@@ -46,19 +45,24 @@ def test_orthogonal_invariance_and_split_identity(pa, big):
     lean = ctx.eval(w, mu, d, False, need_y2=False)
     for key in ("G", "dpsi", "ll"):
         assert np.array_equal(lean[key], full[key]), key
-    ctx.set_y_stage("f64")
+    # the default (int8-digit) Y stage: loss-only try + completion == fused pass
+    assert ctx.int8_passes >= 2
     loss_only, kept, done = ctx.eval_split(w, mu, d, False, need_y2=False)
     assert np.array_equal(loss_only["ll"], full["ll"])
     for key in ("G", "dpsi", "ll"):
         assert np.array_equal(done[key], full[key]), key
-    ctx.set_y_stage("auto")
+    # the fp64 Y stage: the same identities, and agreement with the int8 stage to 1e-13
+    ctx.set_y_stage("f64")
     n8 = ctx.int8_passes
-    lo8, _, done8 = ctx.eval_split(w, mu, d, False, need_y2=True)
-    assert ctx.int8_passes == n8 + 1
-    assert np.max(np.abs(lo8["ll"] - full["ll"])) <= 1e-13 * np.max(np.abs(full["ll"]))
-    assert abs(lo8["y2"].sum() / (N * T) - 1.0) < 1e-10
+    full64 = ctx.eval(w, mu, d, False, need_y2=True)
+    assert abs(full64["y2"].sum() / (N * T) - 1.0) < 1e-10
+    lo64, _, done64 = ctx.eval_split(w, mu, d, False, need_y2=False)
+    assert ctx.int8_passes == n8
+    assert np.array_equal(lo64["ll"], full64["ll"])
     for key in ("G", "dpsi", "ll"):
-        assert np.max(np.abs(done8[key] - full[key])) <= 1e-13 * np.max(np.abs(full[key])), key
+        assert np.array_equal(done64[key], full64[key]), key
+        assert np.max(np.abs(full64[key] - full[key])) <= 1e-13 * np.max(np.abs(full64[key])), key
+    ctx.set_y_stage("auto")
     # tanh: 0 < ψ′ ≤ α and ℓ ≥ |y| ≥ 0 per sample, so the row sums are bounded
     assert np.all(full["dpsi"] > 0) and np.all(full["dpsi"] <= T)
     assert np.all(full["ll"] > 0)
