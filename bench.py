@@ -39,6 +39,10 @@ sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (spec; MI355X_MICROARCH.md); measured 78.0
 HBM_PEAK_GBS = 8000.0
+# i8 MFMA: v_mfma_i32_16x16x64_i8 = 32768 ops per 16 cycles per SIMD (MI355X_MICROARCH.md
+# "I8: 2x BF16 per clock"; 16 cycles/MFMA confirmed by SQ_VALU_MFMA_BUSY_CYCLES) at 2.4 GHz
+I8_MFMA_PEAK_TOPS = 32768 / 16 * 1024 * 2.4e9 / 1e12   # = 5033
+OZ_PRODUCTS = 28   # digit products per multiply-add of the int8-digit Y stage (ozaki.inc)
 
 
 def parse():
@@ -184,6 +188,7 @@ def main():
     t_warm = time.perf_counter() - t_warm
     ctx.kernel_stats(reset=True)
     ctx.kernel_breakdown(reset=True)
+    int8_before = ctx.int8_passes
     passes = 0
     t0 = time.perf_counter()
     steps_run = 0
@@ -197,6 +202,7 @@ def main():
     elapsed = time.perf_counter() - t0
     _, call_ms, _ = ctx.kernel_stats(reset=False)
     brk = ctx.kernel_breakdown(reset=False)
+    int8_timed = ctx.int8_passes - int8_before
 
     if dist is not None:
         import torch
@@ -234,9 +240,14 @@ def main():
     value = T * steps / elapsed
     t_local = ctx.n_local
     # roofline of the dominant kernel (by time per step) — the fused pass
-    # (4N²T flop: Y = W·X and G = ψ·Yᵀ) or the loss-only try (2N²T flop: Y = W·X);
-    # both read the resident X shard once (8·N·T bytes). HIP-event durations on
-    # the solver's stream, averaged over the timed region.
+    # (4N²T algorithmic flop: Y = W·X and G = ψ·Yᵀ) or the loss-only try (2N²T flop:
+    # Y = W·X); both read the resident X shard once (8·N·T bytes). HIP-event
+    # durations on the solver's stream, averaged over the timed region.
+    # With the int8-digit Y stage Y = W·X executes OZ_PRODUCTS exact
+    # i8 digit products per fp64 multiply-add on the i8 matrix cores, G stays on
+    # fp64 MFMA: `peak` is the fp64-equivalent rate of that instruction mix at the
+    # i8 and fp64 MFMA issue peaks, so frac = ideal time / measured time;
+    # `frac_of_fp64_mfma_peak` is the algorithmic rate against 78.6 TF alone.
     pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
@@ -247,8 +258,9 @@ def main():
                 pmc = p.get("kernels", {})
         except Exception:
             pass
-    kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2>", 4.0),
-             "loss": ("k_eval_loss", "k_eval_loss2<tanh,nostore,noY2>", 2.0)}
+    i8 = int8_timed > 0
+    kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2" + (",i8-digit Y>" if i8 else ">"), 4.0),
+             "loss": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2>" if i8 else "k_eval_loss2<tanh,nostore,noY2>", 2.0)}
     rooflines = []
     for kind, (short, label, c) in kinds.items():
         ms, nl = brk.get(kind, (0.0, 0))
@@ -258,19 +270,29 @@ def main():
         flops = c * n * n * t_local
         bytes_alg = 8.0 * n * t_local
         tf = flops / (avg * 1e-3) / 1e12
-        rooflines.append({"bound": "mfma", "achieved": tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                          "frac": tf / FP64_MFMA_PEAK_TFLOPS,
+        if i8:  # executed: Y stage as i8 digit products, G (fused only) on fp64 MFMA
+            i8_ops = OZ_PRODUCTS * 2.0 * n * n * t_local
+            f64_ops = flops - 2.0 * n * n * t_local
+            ideal_s = i8_ops / (I8_MFMA_PEAK_TOPS * 1e12) + f64_ops / (FP64_MFMA_PEAK_TFLOPS * 1e12)
+            peak = flops / ideal_s / 1e12
+            executed = {"i8_ops_per_launch": i8_ops, "fp64_mfma_flops_per_launch": f64_ops,
+                        "ideal_ms_at_issue_peaks": ideal_s * 1e3, "i8_peak_tops": I8_MFMA_PEAK_TOPS,
+                        "fp64_peak_tflops": FP64_MFMA_PEAK_TFLOPS}
+        else:
+            peak, executed = FP64_MFMA_PEAK_TFLOPS, {"fp64_mfma_flops_per_launch": flops}
+        rooflines.append({"bound": "mfma", "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp64-equivalent)",
+                          "frac": tf / peak, "frac_of_fp64_mfma_peak": tf / FP64_MFMA_PEAK_TFLOPS,
                           "traffic": pmc.get(short, {}).get("hbm_bytes_per_launch"),
                           "kernel": label, "avg_kernel_ms": avg, "launches": nl, "ms_per_step": ms / steps,
                           "algorithmic_flops_per_launch": flops, "algorithmic_bytes_per_launch": bytes_alg,
-                          "hbm_gbs_algorithmic": bytes_alg / (avg * 1e-3) / 1e9})
+                          "executed": executed, "hbm_gbs_algorithmic": bytes_alg / (avg * 1e-3) / 1e9})
     rooflines.sort(key=lambda r: -r["ms_per_step"])
     roof = rooflines[0] if rooflines else None
     out = {
         "metric": "samples/sec per Picard-O iter at N=128, T=1e8; iters to tol=1e-7",
         "value": value, "unit": "samples/s per iteration", "n_gpus": world, "steps": steps_run,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic (benches/benchmarks.rs LCG mixture, seed 42, in HBM)",
+        "vs_baseline": None, "dtype": "f64" + (" (Y = W·X from exact i8 digit products)" if i8 else ""), "data": "synthetic (benches/benchmarks.rs LCG mixture, seed 42, in HBM)",
         "config": {"workload": f"Picard-O extended tanh, N={n} sources, T={T} samples (BASELINE configs[2])",
                    "n_sources": n, "n_samples": T, "ortho": True, "extended": True, "density": "tanh(1)",
                    "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass"},

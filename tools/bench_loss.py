@@ -38,3 +38,11 @@ for mode in modes:
     fl = 2.0 * n * n * t
     print(f"{mode:5s} N={n} T={t}: loss kernel {avg:.3f} ms  {fl / avg / 1e9:.2f} TF/s-equiv "
           f"({fl / avg / 1e9 / 78.6 * 100:.1f}% of fp64 78.6)  int8 passes {ctx.int8_passes}", flush=True)
+    ctx.eval(w, mu, d, False, need_y2=False)
+    ctx.kernel_breakdown(reset=True)
+    for _ in range(reps):
+        ctx.eval(w, mu, d, False, need_y2=False)
+    ms, nl = ctx.kernel_breakdown()["fused"]
+    avg = ms / max(nl, 1)
+    print(f"{mode:5s} N={n} T={t}: fused kernel {avg:.3f} ms  {2 * fl / avg / 1e9:.2f} TF/s-equiv "
+          f"({2 * fl / avg / 1e9 / 78.6 * 100:.1f}% of fp64 78.6)", flush=True)

@@ -10,7 +10,8 @@ if d.get("whole_fit"):
     print("whole fit %.4g samples/s/iter  %.2f s  %.2f passes/iter" % (w["samples_per_s_per_iter"], w["iterations_s"],
                                                                      w["passes_per_iter"]))
 for r in d.get("roofline_kernels", []):
-    print("  %-36s %8.2f ms  %.3f of peak  traffic %s" % (r["kernel"], r["avg_kernel_ms"], r["frac"], r["traffic"]))
+    print("  %-44s %8.2f ms  %.3f of peak %.1f (%.3f of fp64 MFMA)  traffic %s" % (
+        r["kernel"], r["avg_kernel_ms"], r["frac"], r["peak"], r.get("frac_of_fp64_mfma_peak", r["frac"]), r["traffic"]))
 for k, c in (d.get("other_configs") or {}).items():
     print("  %s %-48s iters %4d  setup %.2fs  iter %.2fs  %.3g samples/s/iter  passes %d  amari %.2e" % (
         k, c["workload"], c["iters_to_tol"], c["setup_s"], c["iterations_s"], c["samples_per_s_per_iter"],
