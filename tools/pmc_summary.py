@@ -27,7 +27,8 @@ def main():
                     tmpl = name.split("<")[1] if "<" in name else ""
                     if short in name and (tmpl.startswith("8, ") or
                                           (short == "k_eval_fused" and "k_eval_fused_ws<0," in name) or
-                                          (short == "k_eval_loss" and "k_eval_loss2<0, false," in name)):
+                                          (short == "k_eval_loss" and ("k_eval_loss2<0, false," in name or
+                                                                       "k_eval_loss_oz<0, false," in name))):
                         vals[(short, name.split("(")[0])][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {"n": n, "t_local": t_local, "sources": sys.argv[4:], "kernels": {}}
     for short in KERNELS:
