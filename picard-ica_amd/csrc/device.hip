@@ -2074,6 +2074,7 @@ struct DeviceCtx : Evaluator {
     raw_sums_.clear();
     release_xsl();  // a new X: its slice image is rebuilt on demand
     xsl_failed_ = false;
+    wsl_nc_ = 0;    // … and W is sliced again (n_features may change)
     ldx = (n_local + 127) / 128 * 128;  // a fused-pass tile (≤ 128 samples) never crosses a row end
     if (ldx == 0) ldx = 128;
     HIP_OK(hipMalloc(&X, nf * ldx * sizeof(double) + 256));
@@ -2716,26 +2717,47 @@ struct DeviceCtx : Evaluator {
     xsl_valid_ = true;
     return true;
   }
-  // W (nc × nf, host) → slice image [wave][a][kstep][lane][16 B] + row scales 2^(f_i − 12)
+  // W (nc × nf, host) → slice image [wave][a][kstep][lane][16 B] + row scales 2^(f_i − 12).
+  // The same W as the last call (a completion at the W of the loss-only try) is not
+  // sliced again. Digits: oz_digits' arithmetic with a 1.5·2^52 shifter for rint
+  // (exact round-half-even for |v| < 2^51, no libm call on the host).
+  std::vector<double> wsl_w_;
+  size_t wsl_nc_ = 0;
   void upload_wsl(const double* w, size_t nc) {
+    if (wsl_nc_ == nc && wsl_w_.size() == nc * nf && std::memcmp(wsl_w_.data(), w, nc * nf * sizeof(double)) == 0)
+      return;
     constexpr size_t IMG = (size_t)8 * OZ_SLICES * 2 * 64 * 16;
     std::vector<uint8_t> img(IMG, 0);
     std::vector<double> sc(128, 0x1p-12);
+    constexpr double SH = 0x1.8p52;
     for (size_t i = 0; i < nc; ++i) {
       double mx = 0.0;
       for (size_t k = 0; k < nf; ++k) mx = std::fmax(mx, std::fabs(w[i * nf + k]));
       int e = 0;
       if (mx > 0.0) (void)std::frexp(mx, &e);
       sc[i] = std::ldexp(1.0, e - 12);
+      const bool tiny = 6 - e > 1000;  // a row of subnormal size: 2^(6 − e) would overflow
+      const double s6 = tiny ? 0.0 : std::ldexp(1.0, 6 - e);
       const size_t wave = i >> 4, n = i & 15;
       for (size_t k = 0; k < nf; ++k) {
+        double v = tiny ? std::ldexp(w[i * nf + k], 6 - e) : w[i * nf + k] * s6;
         int dg[OZ_SLICES];
-        oz_digits(std::ldexp(w[i * nf + k], 6 - e), dg);
+        for (int a = 0; a < OZ_SLICES; ++a) {
+          const double r = (v + SH) - SH;
+          dg[a] = (int)r;
+          v = (v - r) * 256.0;
+        }
+        for (int a = OZ_SLICES - 1; a > 0; --a) {
+          if (dg[a] > 127) { dg[a] -= 256; dg[a - 1] += 1; }
+          else if (dg[a] < -128) { dg[a] += 256; dg[a - 1] -= 1; }
+        }
         const size_t s = k >> 6, lane = n + 16 * ((k >> 4) & 3), j = k & 15;
         for (int a = 0; a < OZ_SLICES; ++a)
           img[(((wave * OZ_SLICES + a) * 2 + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
       }
     }
+    wsl_w_.assign(w, w + nc * nf);
+    wsl_nc_ = nc;
     if (!d_wsl) {
       HIP_OK(hipMalloc(&d_wsl, IMG));
       HIP_OK(hipMalloc(&d_wsc, 128 * sizeof(double)));
