@@ -117,6 +117,8 @@ def test_shard_sums_match_world1(pa, world, nf):
     ll_w, y2_w = full.eval_loss_multi(w, z, al, mu, pa.DensityType.tanh())
     ll_g, y2_g = g.sum(lambda c: c.eval_loss_multi(w, z, al, mu, pa.DensityType.tanh()))
     assert rel_err(ll_g, ll_w) <= TOL and rel_err(y2_g, y2_w) <= TOL
+    if 64 < nf <= 128:  # these passes ran on each shard's own int8 digit image
+        assert full.int8_passes > 0 and all(c.int8_passes > 0 for c in g.ctxs)
     # sources: per-sample, so every shard is bit-identical to its slice
     y_w = full.sources(w[: min(nf, 32)], mu)
     y_g = np.concatenate([c.sources(w[: min(nf, 32)], mu) for c in g.ctxs], axis=1)
@@ -164,3 +166,22 @@ def test_sharded_fit_reproduces_world1(pa, world, ortho):
         assert abs(am(got.full_unmixing(), a) - am(ref.full_unmixing(), a)) <= 1e-6
         assert am(got.full_unmixing(), np.linalg.inv(ref.full_unmixing())) <= 1e-6
     assert np.max(np.abs(got.whitening - ref.whitening)) <= 1e-10
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fit_int8_stage_reproduces_world1(pa, world):
+    """Picard-O at N = 96 (the int8-digit Y stage: per-sample exponents, so every shard's
+    y values are those of the world=1 context and only the summation order differs):
+    same iteration count, unmixing within 1e-10."""
+    nf, T = 96, 60013
+    full = pa.DeviceContext(0)
+    full.generate(nf, T, 42)
+    x = full.download()
+    cfg = pa.PicardConfig(w_init=np.eye(nf), max_iter=200)
+    ref = pa.Picard.fit_with_config(x, cfg)
+    g = ShardGroup(pa, world, nf, T, seed=42)
+    got = g.fit(cfg)
+    assert all(c.int8_passes > 0 for c in g.ctxs)
+    assert got.converged and ref.converged
+    assert got.n_iterations == ref.n_iterations
+    assert np.max(np.abs(got.unmixing - ref.unmixing)) <= 1e-10
