@@ -43,6 +43,7 @@ HBM_PEAK_GBS = 8000.0
 # "I8: 2x BF16 per clock"; 16 cycles/MFMA confirmed by SQ_VALU_MFMA_BUSY_CYCLES) at 2.4 GHz
 I8_MFMA_PEAK_TOPS = 32768 / 16 * 1024 * 2.4e9 / 1e12   # = 5033
 OZ_PRODUCTS = 28   # digit products per multiply-add of the int8-digit Y stage (ozaki.inc)
+OZ_SCREEN_PRODUCTS = 15   # … of the line-search screen (diagonals D <= 4)
 
 
 def parse():
@@ -189,6 +190,7 @@ def main():
     ctx.kernel_stats(reset=True)
     ctx.kernel_breakdown(reset=True)
     int8_before = ctx.int8_passes
+    ctx.screen_stats(reset=True)
     passes = 0
     t0 = time.perf_counter()
     steps_run = 0
@@ -203,6 +205,7 @@ def main():
     _, call_ms, _ = ctx.kernel_stats(reset=False)
     brk = ctx.kernel_breakdown(reset=False)
     int8_timed = ctx.int8_passes - int8_before
+    brk["screen"] = ctx.screen_stats(reset=False)
 
     if dist is not None:
         import torch
@@ -260,7 +263,8 @@ def main():
             pass
     i8 = int8_timed > 0
     kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2" + (",i8-digit Y>" if i8 else ">"), 4.0),
-             "loss": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2>" if i8 else "k_eval_loss2<tanh,nostore,noY2>", 2.0)}
+             "loss": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2>" if i8 else "k_eval_loss2<tanh,nostore,noY2>", 2.0),
+             "screen": ("k_eval_screen", "k_eval_loss_oz<tanh,nostore,noY2,D<=4> (line-search screen)", 2.0)}
     rooflines = []
     for kind, (short, label, c) in kinds.items():
         ms, nl = brk.get(kind, (0.0, 0))
@@ -271,7 +275,7 @@ def main():
         bytes_alg = 8.0 * n * t_local
         tf = flops / (avg * 1e-3) / 1e12
         if i8:  # executed: Y stage as i8 digit products, G (fused only) on fp64 MFMA
-            i8_ops = OZ_PRODUCTS * 2.0 * n * n * t_local
+            i8_ops = (OZ_SCREEN_PRODUCTS if kind == "screen" else OZ_PRODUCTS) * 2.0 * n * n * t_local
             f64_ops = flops - 2.0 * n * n * t_local
             ideal_s = i8_ops / (I8_MFMA_PEAK_TOPS * 1e12) + f64_ops / (FP64_MFMA_PEAK_TFLOPS * 1e12)
             peak = flops / ideal_s / 1e12
@@ -296,7 +300,8 @@ def main():
         "config": {"workload": f"Picard-O extended tanh, N={n} sources, T={T} samples (BASELINE configs[2])",
                    "n_sources": n, "n_samples": T, "ortho": True, "extended": True, "density": "tanh(1)",
                    "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass"},
-        "passes_per_iter": passes / steps, "iters_to_tol": iters_to_tol, "converged": converged,
+        "passes_per_iter": passes / steps, "screen_passes_per_iter": brk["screen"][1] / steps,
+        "iters_to_tol": iters_to_tol, "converged": converged,
         "total_passes_to_tol": total_passes,
         "whole_fit": ({"samples_per_s_per_iter": T * iters_to_tol / (t_warm + elapsed + t_tol),
                        "iterations_s": t_warm + elapsed + t_tol, "passes_per_iter": total_passes / iters_to_tol,

@@ -275,11 +275,26 @@ void pc_ctx_kernel_breakdown(pc_ctx* ctx, double ms[4], uint64_t n[4], int32_t r
  * combined in fp64, so Y carries the accuracy of an fp64 GEMM (DESIGN.md §3,
  * the Ozaki scheme); the digit image costs another 7 bytes per element of HBM. PC_YSTAGE_F64: every pass on the
  * fp64 MFMA Y stage. Either way the statistics agree with the fp64 oracle to
- * 1e-12 relative; they are bit-identical only within one mode. */
-enum { PC_YSTAGE_AUTO = 0, PC_YSTAGE_F64 = 1 };
+ * 1e-12 relative; they are bit-identical only within one mode.
+ * Under PC_YSTAGE_AUTO the orthogonal solver also SCREENS its loss-only
+ * line-search tries: a pass on the 5 leading digit diagonals (15 digit products)
+ * plus a rigorous bound on the exact Σℓ rejects a try when no exact value could
+ * accept it (core.rs:127-140 decides the same way); every other try runs the
+ * exact pass. PC_YSTAGE_INT8_EXACT: the int8 stage without the screen (every
+ * try exact) — the fits are bit-identical to AUTO's. */
+enum { PC_YSTAGE_AUTO = 0, PC_YSTAGE_F64 = 1, PC_YSTAGE_INT8_EXACT = 2 };
 int pc_ctx_set_y_stage(pc_ctx* ctx, int32_t mode);
 /* number of passes whose Y stage ran on the int8 slices since the context was created */
 uint64_t pc_ctx_int8_passes(const pc_ctx* ctx);
+/* The line-search screen itself: ll_out[i] = Σℓ of row i from the 5 leading digit
+ * diagonals, bound_out[i] ≥ |Σℓ_exact − ll_out[i]| (rounding included), both summed
+ * over ranks. Returns PC_ERR_COMPUTATION when the context has no screen for this
+ * shape / density (int8 stage off, nc outside (64, 128], n_features > 128, cube,
+ * α ≤ 0). */
+int pc_ctx_eval_loss_screen(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, pc_density density,
+                            double* ll_out, double* bound_out, char* err, size_t errlen);
+/* line-search screen passes since the last reset: summed HIP-event kernel ms and count */
+void pc_ctx_screen_stats(pc_ctx* ctx, double* kernel_ms, uint64_t* n_launches, int32_t reset);
 /* hipDeviceSynchronize on `device` (bench bracketing). */
 int pc_device_synchronize(int32_t device);
 

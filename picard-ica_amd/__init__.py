@@ -176,6 +176,8 @@ def _load():
         "pc_ctx_kernel_breakdown": (None, [vp, d, P(u64), i32]),
         "pc_ctx_set_y_stage": (C.c_int, [vp, i32]),
         "pc_ctx_int8_passes": (u64, [vp]),
+        "pc_ctx_screen_stats": (None, [vp, d, P(u64), i32]),
+        "pc_ctx_eval_loss_screen": (C.c_int, [vp, d, u64, d, _Density, d, d, cp, sz]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -199,7 +201,7 @@ EXPORTED = [
     "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 
@@ -605,8 +607,26 @@ class DeviceContext:
         return {k: (ms[i], n[i]) for i, k in enumerate(("fused", "loss", "fromy", "multi"))}
 
     def set_y_stage(self, mode: str = "auto"):
-        """pc_ctx_set_y_stage: "auto" (int8-slice Y stage where the shape allows) or "f64"."""
-        _raise(lib.pc_ctx_set_y_stage(self.h, {"auto": 0, "f64": 1}[mode]), _errbuf())
+        """pc_ctx_set_y_stage: "auto" (int8-digit Y stage where the shape allows, line-search
+        screen on), "f64", or "int8-exact" (int8 stage, every try evaluated exactly)."""
+        _raise(lib.pc_ctx_set_y_stage(self.h, {"auto": 0, "f64": 1, "int8-exact": 2}[mode]), _errbuf())
+
+    def eval_loss_screen(self, w, mu=None, density: DensityType = DensityType()):
+        """pc_ctx_eval_loss_screen: (Σℓ from the screen, bound on |Σℓ_exact − Σℓ_screen|), each [nc]."""
+        w = _c64(w)
+        nc = w.shape[0]
+        mu_a = _c64(mu) if mu is not None else None
+        ll, bnd = np.empty(nc), np.empty(nc)
+        err = _errbuf()
+        _raise(lib.pc_ctx_eval_loss_screen(self.h, _ptr(w), nc, _ptr(mu_a) if mu_a is not None else None,
+                                           density._c(), _ptr(ll), _ptr(bnd), err, len(err)), err)
+        return ll, bnd
+
+    def screen_stats(self, reset: bool = False):
+        """pc_ctx_screen_stats: (Σ screen-pass kernel ms, screen passes) since the last reset."""
+        ms, n = C.c_double(), C.c_uint64()
+        lib.pc_ctx_screen_stats(self.h, C.byref(ms), C.byref(n), int(reset))
+        return ms.value, n.value
 
     @property
     def int8_passes(self) -> int:

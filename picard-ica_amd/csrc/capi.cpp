@@ -29,6 +29,7 @@ void device_synchronize(int device);
 void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset);
 void device_ctx_set_y_stage(Evaluator* e, int mode);
 uint64_t device_ctx_int8_passes(const Evaluator* e);
+void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset);
 }  // namespace pcamd
 
 using namespace pcamd;
@@ -394,12 +395,24 @@ void pc_ctx_kernel_breakdown(pc_ctx* c, double ms[4], uint64_t n[4], int32_t res
 }
 
 int pc_ctx_set_y_stage(pc_ctx* c, int32_t mode) {
-  if (mode != PC_YSTAGE_AUTO && mode != PC_YSTAGE_F64) return PC_ERR_INVALID_CONFIG;
+  if (mode != PC_YSTAGE_AUTO && mode != PC_YSTAGE_F64 && mode != PC_YSTAGE_INT8_EXACT) return PC_ERR_INVALID_CONFIG;
   device_ctx_set_y_stage(c->ev.get(), mode);
   return PC_OK;
 }
 
 uint64_t pc_ctx_int8_passes(const pc_ctx* c) { return device_ctx_int8_passes(c->ev.get()); }
+
+int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density density,
+                            double* ll_out, double* bound_out, char* err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!c->ev->eval_loss_screen(w, nc, mu, density, ll_out, bound_out))
+      throw computation_error("no line-search screen for this shape / density");
+  });
+}
+
+void pc_ctx_screen_stats(pc_ctx* c, double* ms, uint64_t* n, int32_t reset) {
+  device_ctx_screen_stats(c->ev.get(), ms, n, reset);
+}
 
 int pc_device_synchronize(int32_t device) {
   try {

@@ -2689,7 +2689,7 @@ struct DeviceCtx : Evaluator {
     xsl_failed_ = true;
   }
   // the shapes the i8 loss kernel covers: 64 < nc ≤ 128, nf ≤ 128, centred X
-  bool oz_shape(size_t nc) const { return y_stage_ == 0 && pick_nb(nc) == 8 && nf <= 128 && nf > 0; }
+  bool oz_shape(size_t nc) const { return y_stage_ != 1 && pick_nb(nc) == 8 && nf <= 128 && nf > 0; }
   bool ensure_xsl() {
     if (xsl_valid_) return true;
     if (xsl_failed_) return false;
@@ -2714,9 +2714,21 @@ struct DeviceCtx : Evaluator {
     const unsigned grid = (unsigned)std::min<uint64_t>(n_blocks, (uint64_t)n_cu * 16);
     k_slice_x<<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     HIP_OK(hipGetLastError());
+    {  // Σ_t 2^e_t of this shard (padding included: it only loosens the screen's bound)
+      const int nwg = (int)std::max<uint64_t>(1, std::min<uint64_t>((ldx + 4095) / 4096, 1024));
+      const uint64_t per = ((ldx + nwg - 1) / nwg + 511) / 512 * 512;
+      double* part = ensure(d_shift_part, cap_shift_part, (size_t)nwg + 1);
+      k_rowsum<<<dim3((unsigned)((ldx + per - 1) / per), 1), 256, 0, stream>>>(d_xsc, ldx, ldx, 1, per, part);
+      HIP_OK(hipGetLastError());
+      k_sum_slabs<<<1, 256, 0, stream>>>(part, (int)((ldx + per - 1) / per), 1, part + nwg);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(&xsc_sum_, part + nwg, sizeof(double), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+    }
     xsl_valid_ = true;
     return true;
   }
+  double xsc_sum_ = 0.0;
   // W (nc × nf, host) → slice image [wave][a][kstep][lane][16 B] + row scales 2^(f_i − 12).
   // The same W as the last call (a completion at the W of the loss-only try) is not
   // sliced again. Digits: oz_digits' arithmetic with a 1.5·2^52 shifter for rint
@@ -2766,14 +2778,14 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_wsc, sc.data(), 128 * sizeof(double), hipMemcpyHostToDevice, stream));
     HIP_OK(hipStreamSynchronize(stream));  // the host images must outlive the copies
   }
-  template <int D, bool Q>
+  template <int D, bool Q, int DMAX = OZ_SLICES - 1>
   void launch_loss_oz(double alpha, bool store, double* st_rows) {
     const uint64_t n_blocks = (n_local_ + 15) / 16;
     uint64_t bpw;
     const int nwg = partition(n_blocks, &bpw);
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * 128);
     const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
-    auto kern = store ? k_eval_loss_oz<D, true, Q> : k_eval_loss_oz<D, false, Q>;
+    auto kern = store ? k_eval_loss_oz<D, true, Q, DMAX> : k_eval_loss_oz<D, false, Q, DMAX>;
     static bool attr[2] = {false, false};
     if (!attr[store]) {
       HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2788,6 +2800,66 @@ struct DeviceCtx : Evaluator {
         part, nwg, 2 * 128, 0, 128, (int)kept_nc_pending, 2, st_rows, D, alpha, (double)n_local_, 1);
     HIP_OK(hipGetLastError());
     ++n_int8_passes_;
+    if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
+  }
+  uint64_t n_screen_passes_ = 0;
+
+  // The orthogonal line-search screen (Evaluator::eval_loss_screen): the loss-only
+  // pass on diagonals D ≤ 4 of the int8 digit stage (15 digit products instead of
+  // 28). The exact stage's y differs from it by 2^(f_i+e_t−12)·Σ_{D=5,6} 256^−D·P_D,
+  // |P_D| ≤ nf·Σ_{a+b=D} |d_a|max·|d_b|max (|d_0| ≤ 65, |d_a| ≤ 128), so with ℓ
+  // Lipschitz in y (tanh: |ℓ′| = |tanh αy| ≤ 1; exp: |ℓ′| ≤ 1/√(αe)) each row's Σℓ
+  // moves by at most Lip·2^(f_i−12)·B·Σ_t 2^e_t; 1e-10 of Σ_t|ℓ| covers the rounding
+  // of both passes (their sums run in the same order). Ortho densities tanh / exp.
+  static constexpr int OZ_SCREEN_DMAX = 4;
+  bool eval_loss_screen(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+                        double* bound_out) override {
+    if (y_stage_ != 0 || !oz_shape(nc) || !(d.alpha > 0.0) || (d.kind != DENS_TANH && d.kind != DENS_EXP))
+      return false;
+    HIP_OK(hipSetDevice(device));
+    const double* dmu = resident_mu(mu);
+    if (dmu != nullptr || !ensure_xsl()) return false;
+    upload_wsl(w, nc);
+    d_wsl_ready_ = true;
+    double* st_rows = ensure(d_stats, cap_stats, 2 * nc);
+    kept_nc_pending = nc;
+    HIP_OK(hipEventRecord(ev[0], stream));
+    if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
+    else launch_loss_oz<DENS_EXP, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
+    // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
+    double bsum = 0.0;
+    for (int dd = OZ_SCREEN_DMAX + 1; dd <= 2 * (OZ_SLICES - 1); ++dd) {
+      double pm = 0.0;
+      for (int a = 0; a < OZ_SLICES; ++a) {
+        const int b = dd - a;
+        if (b < 0 || b >= OZ_SLICES) continue;
+        pm += (a == 0 ? 65.0 : 128.0) * (b == 0 ? 65.0 : 128.0);
+      }
+      if (dd <= OZ_SLICES - 1) bsum += std::ldexp(pm, -8 * dd);  // only D ≤ 6 are in the exact stage
+    }
+    const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
+    const double tail = (double)nf * bsum * xsc_sum_ * lip;
+    std::vector<double> bnd(nc);
+    for (size_t i = 0; i < nc; ++i) {
+      double mx = 0.0;
+      for (size_t k = 0; k < nf; ++k) mx = std::fmax(mx, std::fabs(w[i * nf + k]));
+      int e = 0;
+      if (mx > 0.0) (void)std::frexp(mx, &e);
+      bnd[i] = std::ldexp(tail, e - 12) * (1.0 + 1e-12);
+    }
+    HIP_OK(hipMemcpyAsync(st_rows + nc, bnd.data(), nc * sizeof(double), hipMemcpyHostToDevice, stream));
+    allreduce(st_rows, 2 * nc);
+    std::vector<double> tmp(2 * nc);
+    HIP_OK(hipMemcpyAsync(tmp.data(), st_rows, 2 * nc * sizeof(double), hipMemcpyDeviceToHost, stream));
+    finish_timing(true, 4);
+    // the rounding slack: Σ_t |ℓ| ≤ |Σℓ| for tanh (ℓ ≥ 0), ≤ n/α for exp (|ℓ| ≤ 1/α)
+    const double n_all = (double)n_total;
+    for (size_t i = 0; i < nc; ++i) {
+      ll_out[i] = tmp[i];
+      const double abs_l = d.kind == DENS_TANH ? std::fabs(tmp[i]) : n_all / d.alpha;
+      bound_out[i] = tmp[nc + i] + 1e-10 * abs_l;
+    }
+    return true;
   }
 
   template <int NB, int D, bool Q>
@@ -2852,7 +2924,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
   }
 
-  double sum_loss_ms = 0, sum_fromy_ms = 0, sum_multi_ms = 0;
+  double sum_loss_ms = 0, sum_fromy_ms = 0, sum_multi_ms = 0, sum_screen_ms = 0;
+  uint64_t n_screen = 0;
   uint64_t n_multi = 0;
   uint64_t n_loss = 0, n_fromy = 0;
   void finish_timing(bool kernel_timed, int kind = 0) {
@@ -2868,6 +2941,7 @@ struct DeviceCtx : Evaluator {
     if (kind == 1) { sum_loss_ms += a; ++n_loss; }
     if (kind == 2) { sum_fromy_ms += a; ++n_fromy; }
     if (kind == 3) { sum_multi_ms += a; ++n_multi; }
+    if (kind == 4) { sum_screen_ms += a; ++n_screen; }
   }
   double sum_split_ms = 0;
   uint64_t n_split = 0;
@@ -3262,6 +3336,12 @@ void device_ctx_set_y_stage(Evaluator* e, int mode) {
   d->y_stage_ = mode;
 }
 uint64_t device_ctx_int8_passes(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_int8_passes_; }
+void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset) {
+  auto* d = static_cast<DeviceCtx*>(e);
+  *ms = d->sum_screen_ms;
+  *n = d->n_screen;
+  if (reset) { d->sum_screen_ms = 0; d->n_screen = 0; }
+}
 void device_synchronize(int device) {
   HIP_OK(hipSetDevice(device));
   HIP_OK(hipDeviceSynchronize());

@@ -82,6 +82,17 @@ class Evaluator {
     return false;
   }
   virtual void eval_complete(pc_density d, bool need_h, EvalStats* out) { (void)d; (void)need_h; (void)out; }
+  // Orthogonal line-search screen: Σℓ of a CHEAPER approximation of the loss-only
+  // pass at w (ll_out, nc) and, per row, a rigorous bound on how far the exact
+  // pass's Σℓ can lie from it (bound_out, nc; any rounding included), both summed
+  // over ranks. The solver rejects a try without the exact pass only when even
+  // the bound cannot bring its loss below the current one, so no decision of
+  // core.rs:127-140 changes. false = no screen here (the try is evaluated exactly).
+  virtual bool eval_loss_screen(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+                                double* bound_out) {
+    (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
+    return false;
+  }
   // Non-ortho line search: Σℓ and Σy² of Y_j = (W + α_j·Z)·(X−μ) for every α_j
   // in one pass (ll_out, y2_out: [na][nc]). false = not supported here.
   virtual bool eval_loss_multi(const double* w, const double* z, size_t nc, const double* mu, pc_density d,

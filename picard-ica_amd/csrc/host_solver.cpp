@@ -376,7 +376,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
   const size_t n = nc_;
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
-  LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false};
+  LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false, false};
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
@@ -456,13 +456,44 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       }
       no_multi_ = true;  // evaluator cannot: per-try passes from now on
     }
+    r.tries = k + 1;
     if (k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
+    } else if (ortho && !keep_y_) {
+      // Screen (Evaluator::eval_loss_screen): a cheaper pass plus a rigorous bound on
+      // the exact Σℓ. If even the most favourable exact loss cannot beat the current
+      // one, the try fails exactly as core.rs:127-140 would decide; otherwise the exact
+      // evaluation runs as a full pass (it also yields G if the try is accepted).
+      bool rejected = false, screened = false;
+      std::vector<double> ll(n), bnd(n);
+      const Mat wt = matmul(r.w, P_);
+      ev_->want_y2 = false;
+      const double t0 = now_ms();
+      if (ev_->eval_loss_screen(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(), bnd.data())) {
+        screened = true;
+        eval_ms_ += now_ms() - t0;
+        ++screen_passes_;
+        double lo = 0.0;
+        for (size_t i = 0; i < n; ++i) lo += (signs_[i] * ll[i] - std::fabs(signs_[i]) * bnd[i]) / (double)T_;
+        rejected = !(lo < current_loss_);  // exact loss ≥ lo ≥ current: the try fails
+      }
+      if (rejected) {
+        ++screen_rejects_;
+        r.screened_out = true;  // no exact statistics for this W
+        alpha /= 2.0;
+        continue;
+      }
+      if (screened) {
+        evaluate(r.w, &r.stats);
+        r.partial = false;
+      } else {
+        r.partial = evaluate_loss(r.w, &r.stats);
+      }
     } else {
       r.partial = evaluate_loss(r.w, &r.stats);
     }
-    r.tries = k + 1;
+    r.screened_out = false;
     bool singular;
     r.loss = loss_of(r.stats, r.w, signs_, &singular);
     if (r.loss < current_loss_) {
@@ -577,7 +608,7 @@ bool Solver::step() {
     res = line_search(scale(g, -1.0), 10, false, false);
   }
   if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
-  if (res.needs_full) {  // rejected multi-try search kept as the iterate
+  if (res.needs_full || res.screened_out) {  // rejected multi-try / screened last try kept as the iterate
     evaluate(res.w, &res.stats);
     bool singular;
     res.loss = loss_of(res.stats, res.w, signs_, &singular);
@@ -585,9 +616,10 @@ bool Solver::step() {
   if (trace_) {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
-                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f\n",
+                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f screens %llu rejected %llu\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
-                 res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_);
+                 res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_,
+                 (unsigned long long)screen_passes_, (unsigned long long)screen_rejects_);
   }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;

@@ -51,6 +51,8 @@ class Solver {
   uint64_t last_evals() const { return last_evals_; }
   uint64_t total_evals() const { return total_evals_; }
   uint64_t total_completions() const { return total_completions_; }
+  uint64_t screen_passes() const { return screen_passes_; }
+  uint64_t screen_rejects() const { return screen_rejects_; }
 
  private:
   std::unique_ptr<TransformWorker> ahead_;
@@ -60,7 +62,9 @@ class Solver {
   void evaluate(const Mat& w_core, EvalStats* out);
   bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
   void complete(EvalStats* out);
-  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full; };
+  // screened_out: the last try was rejected by the screen alone (no exact stats for w)
+  struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full;
+                    bool screened_out; };
   LsResult line_search(const Mat& direction, size_t tries, bool multi_first, bool first_loss_only);
   void init_core();
   Mat ica_par(const Mat& w_init);
@@ -95,6 +99,7 @@ class Solver {
   bool converged_ = false, done_ = false;
   uint64_t last_evals_ = 0, total_evals_ = 0;
   uint64_t total_completions_ = 0;
+  uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are

@@ -211,3 +211,72 @@ def test_int8_gram_stays_fp64(pa, rng):
     assert ctx.int8_passes == 0
     xc = x - x.mean(axis=1, keepdims=True)
     assert rel_err(g, xc @ xc.T) <= TOL
+
+
+@pytest.mark.parametrize("n", [72, 128])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("tanh", 0.5), ("exp", 1.0), ("exp", 0.3)])
+def test_screen_bound_holds(pa, rng, n, dens):
+    """The line-search screen's bound covers the exact pass: |Σℓ_exact − Σℓ_screen| ≤ bound
+    for every row, over W of very different scales; and it is tight enough to decide
+    (bound ≤ 1e-6 of Σ|ℓ|)."""
+    x = laplace_mix(rng, n, 20011)
+    x[:, 5] *= 1e3  # one loud sample: its exponent dominates its own column only
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    xc = x - mu[:, None]
+    k = np.linalg.cholesky(np.linalg.inv(xc @ xc.T / x.shape[1])).T
+    for scale in (1e-3, 0.3, 1.0, 7.0):
+        w = scale * (np.linalg.qr(rng.normal(size=(n, n)))[0] @ k)
+        ll_s, bnd = ctx.eval_loss_screen(w, mu, d)
+        lo, _, _ = ctx.eval_split(w, mu, d, False, need_y2=False)
+        err = np.abs(lo["ll"] - ll_s)
+        assert np.all(err <= bnd), (scale, np.max(err / bnd))
+        assert np.all(bnd >= 0)
+        if dens[0] == "tanh":
+            assert np.max(bnd / np.abs(lo["ll"])) <= 1e-6, (scale, np.max(bnd / np.abs(lo["ll"])))
+    _, ns = ctx.screen_stats()
+    assert ns == 4
+
+
+def test_screen_unavailable_shapes(pa, rng):
+    x = laplace_mix(rng, 40, 3000)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    with pytest.raises(pa.ComputationError):  # nc ≤ 64: no int8 stage
+        ctx.eval_loss_screen(np.eye(40), x.mean(axis=1), pa.DensityType.tanh())
+    x = laplace_mix(rng, 100, 3000)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    with pytest.raises(pa.ComputationError):  # cube: ℓ not Lipschitz
+        ctx.eval_loss_screen(np.eye(100), x.mean(axis=1), pa.DensityType.cube())
+    ctx.set_y_stage("int8-exact")
+    with pytest.raises(pa.ComputationError):
+        ctx.eval_loss_screen(np.eye(100), x.mean(axis=1), pa.DensityType.tanh())
+
+
+@pytest.mark.parametrize("n,seed", [(128, 42), (96, 7)])
+def test_screened_fit_bit_identical(pa, n, seed, capfd, monkeypatch):
+    """A Picard-O fit with the line-search screen (default) and without it (int8-exact):
+    identical iterations and bit-identical unmixing — the screen rejects only tries the
+    exact pass would reject. The bench mixture (benches/benchmarks.rs) has line searches
+    that fail all 10 tries, so the screen does reject some (counted in the trace)."""
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    res = {}
+    for mode in ("auto", "int8-exact"):
+        ctx = pa.DeviceContext(0)
+        ctx.generate(n, 200003, seed)
+        ctx.set_y_stage(mode)
+        sv = pa.Solver(ctx, pa.PicardConfig(random_state=42, max_iter=60))
+        while not sv.step():
+            pass
+        res[mode] = (sv.finish(), ctx.screen_stats()[1])
+        sv.close()
+    err = capfd.readouterr().err
+    (r, ns), (r0, ns0) = res["auto"], res["int8-exact"]
+    assert ns > 0 and ns0 == 0
+    assert r.n_iterations == r0.n_iterations and r.converged == r0.converged
+    assert np.array_equal(r.unmixing, r0.unmixing)
+    rejected = [int(line.split("rejected ")[1].split()[0]) for line in err.splitlines() if "rejected " in line]
+    assert rejected and max(rejected) > 0

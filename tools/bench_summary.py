@@ -3,8 +3,8 @@ import json
 import sys
 
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print("value %.4g  ms/step %.1f  passes/iter %.2f  iters %s" % (d["value"], d["ms_per_step"], d["passes_per_iter"],
-                                                                d["iters_to_tol"]))
+print("value %.4g  ms/step %.1f  passes/iter %.2f (+%.2f screens)  iters %s" % (
+    d["value"], d["ms_per_step"], d["passes_per_iter"], d.get("screen_passes_per_iter", 0.0), d["iters_to_tol"]))
 if d.get("whole_fit"):
     w = d["whole_fit"]
     print("whole fit %.4g samples/s/iter  %.2f s  %.2f passes/iter" % (w["samples_per_s_per_iter"], w["iterations_s"],
