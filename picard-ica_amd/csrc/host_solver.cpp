@@ -474,9 +474,15 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         screened = true;
         eval_ms_ += now_ms() - t0;
         ++screen_passes_;
-        double lo = 0.0;
-        for (size_t i = 0; i < n; ++i) lo += (signs_[i] * ll[i] - std::fabs(signs_[i]) * bnd[i]) / (double)T_;
+        double lo = 0.0, eb = 0.0;
+        for (size_t i = 0; i < n; ++i) {
+          lo += (signs_[i] * ll[i] - std::fabs(signs_[i]) * bnd[i]) / (double)T_;
+          eb += std::fabs(signs_[i]) * bnd[i] / (double)T_;
+        }
         rejected = !(lo < current_loss_);  // exact loss ≥ lo ≥ current: the try fails
+        if (trace_)
+          std::fprintf(stderr, "[picard-screen] try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", k + 1, alpha,
+                       lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact");
       }
       if (rejected) {
         ++screen_rejects_;
