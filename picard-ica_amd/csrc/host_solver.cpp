@@ -457,10 +457,15 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       no_multi_ = true;  // evaluator cannot: per-try passes from now on
     }
     r.tries = k + 1;
-    if (k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
+    // Orthogonal searches screen every try when the evaluator has a screen (the first
+    // try too: after a try-1 accept it is rejected about half the time on C3, and a
+    // rejected full pass wastes its G stage); otherwise try 1 is a full pass unless the
+    // direction is not a descent direction.
+    const bool screen = ortho && !keep_y_ && screen_ok_;
+    if (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
-    } else if (ortho && !keep_y_) {
+    } else if (screen) {
       // Screen (Evaluator::eval_loss_screen): a cheaper pass plus a rigorous bound on
       // the exact Σℓ. If even the most favourable exact loss cannot beat the current
       // one, the try fails exactly as core.rs:127-140 would decide; otherwise the exact
@@ -494,7 +499,13 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         evaluate(r.w, &r.stats);
         r.partial = false;
       } else {
-        r.partial = evaluate_loss(r.w, &r.stats);
+        screen_ok_ = false;  // this evaluator has no screen: the schedule above from now on
+        if (k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
+          evaluate(r.w, &r.stats);
+          r.partial = false;
+        } else {
+          r.partial = evaluate_loss(r.w, &r.stats);
+        }
       }
     } else {
       r.partial = evaluate_loss(r.w, &r.stats);

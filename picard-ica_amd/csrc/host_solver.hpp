@@ -100,6 +100,7 @@ class Solver {
   uint64_t last_evals_ = 0, total_evals_ = 0;
   uint64_t total_completions_ = 0;
   uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
+  bool screen_ok_ = true;  // false once the evaluator declined a screen (then never asked again)
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are
