@@ -367,7 +367,7 @@ class TransformWorker {
 Solver::~Solver() = default;
 
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first,
-                                     bool first_loss_only) {  // core.rs:99-150
+                                     bool first_loss_only, bool full_first) {  // core.rs:99-150
   // Evaluation schedule: a try is a full fused pass, or a loss-only pass
   // completed (G, H, Σψ′) only if that try becomes the new iterate (both
   // bit-identical). Non-ortho searches evaluate their tries in one multi-α pass
@@ -461,7 +461,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     // try too: after a try-1 accept it is rejected about half the time on C3, and a
     // rejected full pass wastes its G stage); otherwise try 1 is a full pass unless the
     // direction is not a descent direction.
-    const bool screen = ortho && !keep_y_ && screen_ok_;
+    // (full_first: the gradient fallback, whose try 1 is accepted almost always — a
+    // screen pays only below ~2/3 acceptance, 28.5 + 84·p < 84 ms on C3)
+    const bool screen = ortho && !keep_y_ && screen_ok_ && !(k == 0 && full_first);
     if (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
@@ -622,7 +624,7 @@ bool Solver::step() {
   first_full_ = res.success && res.tries == 1;
   if (!res.success) {  // core.rs:349-364
     mem_.clear();
-    res = line_search(scale(g, -1.0), 10, false, false);
+    res = line_search(scale(g, -1.0), 10, false, false, true);
   }
   if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
   if (res.needs_full || res.screened_out) {  // rejected multi-try / screened last try kept as the iterate

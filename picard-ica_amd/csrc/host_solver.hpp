@@ -65,7 +65,8 @@ class Solver {
   // screened_out: the last try was rejected by the screen alone (no exact stats for w)
   struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full;
                     bool screened_out; };
-  LsResult line_search(const Mat& direction, size_t tries, bool multi_first, bool first_loss_only);
+  LsResult line_search(const Mat& direction, size_t tries, bool multi_first, bool first_loss_only,
+                       bool full_first = false);
   void init_core();
   Mat ica_par(const Mat& w_init);
   Mat jade(size_t max_iter, double tol);
