@@ -280,3 +280,26 @@ def test_screened_fit_bit_identical(pa, n, seed, capfd, monkeypatch):
     assert np.array_equal(r.unmixing, r0.unmixing)
     rejected = [int(line.split("rejected ")[1].split()[0]) for line in err.splitlines() if "rejected " in line]
     assert rejected and max(rejected) > 0
+
+
+@pytest.mark.parametrize("t", [16 * 512 * 7 + 5, 1_000_003])
+def test_int8_fused_many_blocks_per_workgroup(pa, po, rng, t):
+    """Many 16-sample blocks per workgroup (the fused pass's pipeline runs its steady
+    state: X staged two blocks ahead into a rotating third buffer): bit-identical to the
+    loss-only pass, and the fp64 stage within 1e-13."""
+    n = 128
+    x = laplace_mix(rng, n, t)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = pa.DensityType.tanh()
+    full = ctx.eval(w, mu, d, False)
+    lo, _, done = ctx.eval_split(w, mu, d, False)
+    assert np.array_equal(lo["ll"], full["ll"])
+    for k in full:
+        assert np.array_equal(done[k], full[k]), k
+    ctx.set_y_stage("f64")
+    ref = ctx.eval(w, mu, d, False)
+    for k in full:
+        assert rel_err(full[k], ref[k]) <= TOL_MODES, (k, rel_err(full[k], ref[k]))
