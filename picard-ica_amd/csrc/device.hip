@@ -2744,7 +2744,15 @@ struct DeviceCtx : Evaluator {
     constexpr double SH = 0x1.8p52;
     for (size_t i = 0; i < nc; ++i) {
       double mx = 0.0;
-      for (size_t k = 0; k < nf; ++k) mx = std::fmax(mx, std::fabs(w[i * nf + k]));
+      bool bad = false;  // a NaN / ±inf weight: the row's scale becomes NaN (y = NaN, as in fp64)
+      for (size_t k = 0; k < nf; ++k) {
+        bad |= !std::isfinite(w[i * nf + k]);
+        mx = std::fmax(mx, std::fabs(w[i * nf + k]));
+      }
+      if (bad) {
+        sc[i] = std::nan("");
+        continue;  // zero digits
+      }
       int e = 0;
       if (mx > 0.0) (void)std::frexp(mx, &e);
       sc[i] = std::ldexp(1.0, e - 12);

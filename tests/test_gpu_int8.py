@@ -303,3 +303,27 @@ def test_int8_fused_many_blocks_per_workgroup(pa, po, rng, t):
     ref = ctx.eval(w, mu, d, False)
     for k in full:
         assert rel_err(full[k], ref[k]) <= TOL_MODES, (k, rel_err(full[k], ref[k]))
+
+
+def test_int8_non_finite_propagates(pa, rng):
+    """A NaN in X or in W reaches the statistics as NaN on the int8 stage, as on the fp64
+    stage (the digit image carries it in the sample / row scale)."""
+    n = 100
+    x = laplace_mix(rng, n, 3000)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    d = pa.DensityType.tanh()
+    for mode in ("auto", "f64"):
+        xb = x.copy()
+        xb[3, 100] = np.nan
+        ctx = pa.DeviceContext(0)
+        ctx.load(xb)
+        ctx.set_y_stage(mode)
+        st = ctx.eval(w, None, d, False)
+        assert np.isnan(st["ll"]).all() and np.isnan(st["G"]).any(), mode
+        ctx = pa.DeviceContext(0)
+        ctx.load(x)
+        ctx.set_y_stage(mode)
+        wb = w.copy()
+        wb[5, 7] = np.inf
+        st = ctx.eval(wb, None, d, False)
+        assert np.isnan(st["ll"][5]) and np.isfinite(st["ll"][6]), mode
