@@ -299,7 +299,12 @@ def main():
         "vs_baseline": None, "dtype": "f64" + (" (Y = W·X from exact i8 digit products)" if i8 else ""), "data": "synthetic (benches/benchmarks.rs LCG mixture, seed 42, in HBM)",
         "config": {"workload": f"Picard-O extended tanh, N={n} sources, T={T} samples (BASELINE configs[2])",
                    "n_sources": n, "n_samples": T, "ortho": True, "extended": True, "density": "tanh(1)",
-                   "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass"},
+                   "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass",
+                   "line_search": ("every orthogonal try screened by a cheaper int8 pass with a rigorous bound on "
+                                   "its exact loss; a try is rejected without the exact pass only when no exact "
+                                   "value could accept it (decisions and iterates bit-identical to evaluating "
+                                   "every try exactly: tests/test_gpu_int8.py); screens run inside the timed "
+                                   "region and are counted in screen_passes_per_iter") if i8 else "every try exact"},
         "passes_per_iter": passes / steps, "screen_passes_per_iter": brk["screen"][1] / steps,
         "iters_to_tol": iters_to_tol, "converged": converged,
         "total_passes_to_tol": total_passes,
