@@ -213,7 +213,10 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   ev_->want_y2 = !cfg_.ortho && extended_;
   const double t0 = now_ms();
   ev_->eval(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
-  eval_ms_ += now_ms() - t0;
+  const double dt = now_ms() - t0;
+  eval_ms_ += dt;
+  full_ms_ += dt;
+  ++n_full_ms_;
   ++last_evals_;
   ++total_evals_;
 }
@@ -457,13 +460,27 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       no_multi_ = true;  // evaluator cannot: per-try passes from now on
     }
     r.tries = k + 1;
-    // Orthogonal searches screen every try when the evaluator has a screen (the first
-    // try too: after a try-1 accept it is rejected about half the time on C3, and a
-    // rejected full pass wastes its G stage); otherwise try 1 is a full pass unless the
-    // direction is not a descent direction.
-    // (full_first: the gradient fallback, whose try 1 is accepted almost always — a
-    // screen pays only below ~2/3 acceptance, 28.5 + 84·p < 84 ms on C3)
-    const bool screen = ortho && !keep_y_ && screen_ok_ && !(k == 0 && full_first);
+    // Orthogonal searches screen their tries when the evaluator has a screen. Try 1 of a
+    // descent direction (⟨g, D⟩ < 0) is accepted with some probability p: screening it
+    // costs t_s + p·t_f against t_f for a full pass, so it is screened only while the
+    // running estimate of p is below 1 − t_s/t_f (measured running means). p is estimated
+    // per state of the previous search (accepted at try 1 or not: on C3 the first tries
+    // alternate, 0.6 vs 1.0 acceptance), Laplace-smoothed over this fit's first tries.
+    // The gradient fallback (full_first) is accepted at try 1 almost always: full pass.
+    // Schedule only: no decision changes.
+    bool screen = ortho && !keep_y_ && screen_ok_;
+    const bool first_policy = k == 0 && !first_loss_only && !full_first;
+    if (screen && k == 0) {
+      if (full_first) {
+        screen = false;
+      } else if (first_policy) {
+        const double ts = n_screen_ms_ ? screen_ms_ / n_screen_ms_ : 28.0;
+        const double tf = n_full_ms_ ? full_ms_ / n_full_ms_ : 83.0;
+        const int st = first_full_ ? 1 : 0;
+        const double p_acc = (first_acc_[st] + 1.0) / (first_n_[st] + 2.0);
+        screen = p_acc < 1.0 - ts / tf;
+      }
+    }
     if (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
       evaluate(r.w, &r.stats);
       r.partial = false;
@@ -479,7 +496,10 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       const double t0 = now_ms();
       if (ev_->eval_loss_screen(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(), bnd.data())) {
         screened = true;
-        eval_ms_ += now_ms() - t0;
+        const double dt = now_ms() - t0;
+        eval_ms_ += dt;
+        screen_ms_ += dt;
+        ++n_screen_ms_;
         ++screen_passes_;
         double lo = 0.0, eb = 0.0;
         for (size_t i = 0; i < n; ++i) {
@@ -492,6 +512,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
                        lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact");
       }
       if (rejected) {
+        if (first_policy) first_n_[first_full_ ? 1 : 0] += 1.0;
         ++screen_rejects_;
         r.screened_out = true;  // no exact statistics for this W
         alpha /= 2.0;
@@ -515,7 +536,12 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     r.screened_out = false;
     bool singular;
     r.loss = loss_of(r.stats, r.w, signs_, &singular);
-    if (r.loss < current_loss_) {
+    const bool accepted = r.loss < current_loss_;
+    if (first_policy) {
+      first_n_[first_full_ ? 1 : 0] += 1.0;
+      if (accepted) first_acc_[first_full_ ? 1 : 0] += 1.0;
+    }
+    if (accepted) {
       r.success = true;
       r.step = scale(direction, alpha);
       return r;
