@@ -38,6 +38,13 @@ for mode in modes:
     fl = 2.0 * n * n * t
     print(f"{mode:5s} N={n} T={t}: loss kernel {avg:.3f} ms  {fl / avg / 1e9:.2f} TF/s-equiv "
           f"({fl / avg / 1e9 / 78.6 * 100:.1f}% of fp64 78.6)  int8 passes {ctx.int8_passes}", flush=True)
+    if mode == "auto":
+        ctx.eval_loss_screen(w, mu, d)
+        ctx.screen_stats(reset=True)
+        for _ in range(reps):
+            ctx.eval_loss_screen(w, mu, d)
+        ms, nl = ctx.screen_stats()
+        print(f"{mode:5s} N={n} T={t}: screen kernel {ms / max(nl, 1):.3f} ms", flush=True)
     ctx.eval(w, mu, d, False, need_y2=False)
     ctx.kernel_breakdown(reset=True)
     for _ in range(reps):
