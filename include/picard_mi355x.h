@@ -251,6 +251,10 @@ typedef struct {
   int (*eval_loss_multi)(void* user, const double* w, const double* z, uint64_t nc, const double* mu,
                          pc_density density, const double* alphas, uint64_t n_alpha, double* ll_out,
                          double* y2_out);
+  /* optional (NULL: no line-search screen): pc_ctx_eval_loss_screen's contract —
+   * Σℓ of an approximation and per-row bounds on its distance to the exact Σℓ */
+  int (*eval_loss_screen)(void* user, const double* w, uint64_t nc, const double* mu, pc_density density,
+                          double* ll_out, double* bound_out);
 } pc_host_evaluator;
 int pc_fit_with_evaluator(const pc_host_evaluator* ev, const pc_config* cfg, pc_result* out,
                           char* err, size_t errlen);

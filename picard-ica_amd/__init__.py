@@ -123,11 +123,15 @@ MultiFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_
                       C.POINTER(C.c_double))
 
 
+ScreenFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_uint64, C.POINTER(C.c_double), _Density,
+                       C.POINTER(C.c_double), C.POINTER(C.c_double))
+
+
 class _HostEvaluator(C.Structure):
     _fields_ = [
         ("user", C.c_void_p), ("n_features", C.c_uint64), ("n_samples", C.c_uint64),
         ("rowsum", RowsumFn), ("gram", GramFn), ("eval", EvalFn), ("sources", SourcesFn),
-        ("moments4", Moments4Fn), ("eval_loss_multi", MultiFn),
+        ("moments4", Moments4Fn), ("eval_loss_multi", MultiFn), ("eval_loss_screen", ScreenFn),
     ]
 
 
@@ -737,13 +741,14 @@ class Solver:
 
 
 def fit_with_host_evaluator(n_features: int, n_samples: int, config: PicardConfig, *, rowsum, gram, eval,
-                            sources, moments4=None, eval_loss_multi=None) -> PicardResult:
+                            sources, moments4=None, eval_loss_multi=None, eval_loss_screen=None) -> PicardResult:
     """Run the host driver over Python callbacks (pc_fit_with_evaluator).
 
     Test hook for the host logic on machines without a GPU, or over detached
     shard contexts on one GPU; the callbacks get numpy arrays and return them
     (see pc_host_evaluator). ``eval_loss_multi(w, z, alphas, mu, density)``
-    returns (Σℓ, Σy²), each [n_alpha, nc]."""
+    returns (Σℓ, Σy²), each [n_alpha, nc]; ``eval_loss_screen(w, mu, density)`` returns
+    (Σℓ of an approximation, per-row bound on its distance to the exact Σℓ), each [nc]."""
     def _rs(user, out):
         o = np.ctypeslib.as_array(out, shape=(n_features,))
         o[:] = rowsum()
@@ -794,9 +799,18 @@ def fit_with_host_evaluator(n_features: int, n_samples: int, config: PicardConfi
         np.ctypeslib.as_array(y2_out, shape=(na * nc,))[:] = np.asarray(y2).reshape(-1)
         return 0
 
+    def _screen(user, w, nc, mu, dens, ll_out, bound_out):
+        W = np.ctypeslib.as_array(w, shape=(nc * n_features,)).reshape(nc, n_features).copy()
+        m = np.ctypeslib.as_array(mu, shape=(n_features,)).copy() if mu else None
+        ll, bnd = eval_loss_screen(W, m, DensityType(dens.kind, dens.alpha))
+        np.ctypeslib.as_array(ll_out, shape=(nc,))[:] = np.asarray(ll).reshape(-1)
+        np.ctypeslib.as_array(bound_out, shape=(nc,))[:] = np.asarray(bnd).reshape(-1)
+        return 0
+
     cbs = (RowsumFn(_rs), GramFn(_gram), EvalFn(_eval), SourcesFn(_src),
            Moments4Fn(_m4) if moments4 is not None else Moments4Fn(),
-           MultiFn(_multi) if eval_loss_multi is not None else MultiFn())
+           MultiFn(_multi) if eval_loss_multi is not None else MultiFn(),
+           ScreenFn(_screen) if eval_loss_screen is not None else ScreenFn())
     ev = _HostEvaluator(None, n_features, n_samples, *cbs)
     c, _keep = config._c()
     r = _Result()

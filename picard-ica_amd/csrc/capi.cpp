@@ -94,6 +94,12 @@ struct CallbackEvaluator : Evaluator {
     chk(cb.eval_loss_multi(cb.user, w, z, nc, mu, d, alphas, (uint64_t)na, ll_out, y2_out), "eval_loss_multi");
     return true;
   }
+  bool eval_loss_screen(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+                        double* bound_out) override {
+    if (!cb.eval_loss_screen) return false;
+    chk(cb.eval_loss_screen(cb.user, w, nc, mu, d, ll_out, bound_out), "eval_loss_screen");
+    return true;
+  }
 };
 
 Mat full_unmixing_of(const pc_result* r) {

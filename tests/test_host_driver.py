@@ -105,3 +105,40 @@ def test_seeded_random_init_is_deterministic(pa, po, c1_data):
     r2 = host_fit(pa, po, x, pa.PicardConfig(random_state=7))
     assert np.array_equal(r1.unmixing, r2.unmixing)
     assert r1.converged and po.amari_distance(r1.full_unmixing(), a) < 0.01
+
+
+@pytest.mark.parametrize("n,t,extended", [(16, 20000, True), (12, 15000, False)])
+def test_screened_line_search_decisions_unchanged(pa, po, dg, n, t, extended):
+    """The orthogonal line-search screen (Evaluator::eval_loss_screen) changes no decision:
+    with a screen that returns the exact Σℓ moved anywhere inside its stated bound, the fit
+    is bit-identical to the unscreened one (same iterations, same unmixing bits), the screen
+    rejects tries (fewer exact passes) and no try is rejected that the exact pass accepts."""
+    x, _ = dg.generate_data(n, t, 42)[:2]
+    rng = np.random.default_rng(0)
+    calls = {"screen": 0, "eval": 0}
+
+    def ev(w, mu, d, need_h):
+        calls["eval"] += 1
+        return po.pass_stats(w, mu, x, density_of(po, d), need_h)
+
+    def screen(w, mu, d):
+        calls["screen"] += 1
+        ll = po.pass_stats(w, mu, x, density_of(po, d), False)["ll"]
+        bnd = 1e-9 * np.abs(ll) + 1e-12
+        return ll + rng.uniform(-0.9, 0.9, size=ll.shape) * bnd, bnd
+
+    def fit(with_screen):
+        calls.update(screen=0, eval=0)
+        kw = dict(eval_loss_screen=screen) if with_screen else {}
+        r = pa.fit_with_host_evaluator(
+            x.shape[0], x.shape[1], pa.PicardConfig(random_state=42, extended=extended, max_iter=60),
+            rowsum=lambda: x.sum(axis=1), gram=lambda mu: (x - mu[:, None]) @ (x - mu[:, None]).T,
+            eval=ev, sources=lambda w, mu: w @ (x - mu[:, None]), **kw)
+        return r, dict(calls)
+
+    r0, c0 = fit(False)
+    r1, c1 = fit(True)
+    assert c0["screen"] == 0 and c1["screen"] > 0
+    assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
+    assert np.array_equal(r1.unmixing, r0.unmixing)
+    assert c1["eval"] < c0["eval"]  # rejected tries ran no exact pass
