@@ -2811,6 +2811,26 @@ struct DeviceCtx : Evaluator {
     if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
   }
   uint64_t n_screen_passes_ = 0;
+  // Rank agreement on a per-rank capability that selects between branches with different
+  // collectives: the first call all-reduces the local flag (all ranks must have it);
+  // later calls reuse the answer, and a rank that loses the capability afterwards
+  // raises instead of diverging. state: 0 not asked, 1 all have it, -1 some do not.
+  int screen_agreed_ = 0, ybuf_agreed_ = 0;
+  bool agree_once(int& state, bool local) {
+    if (state == 0) {
+      double* f = ensure(d_shift_sum, cap_shift_sum, std::max<size_t>(nf, 1));  // scratch (not d_stats)
+      const double one = local ? 1.0 : 0.0;
+      HIP_OK(hipMemcpyAsync(f, &one, sizeof(double), hipMemcpyHostToDevice, stream));
+      allreduce(f, 1);
+      double all = 0.0;
+      HIP_OK(hipMemcpyAsync(&all, f, sizeof(double), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      state = all == (double)world ? 1 : -1;
+    }
+    if (state < 0) return false;
+    if (!local) throw computation_error("a capability the ranks agreed on (int8 digit image / kept Y) was lost on this rank");
+    return true;
+  }
 
   // The orthogonal line-search screen (Evaluator::eval_loss_screen): the loss-only
   // pass on diagonals D ≤ 4 of the int8 digit stage (15 digit products instead of
@@ -2826,7 +2846,12 @@ struct DeviceCtx : Evaluator {
       return false;
     HIP_OK(hipSetDevice(device));
     const double* dmu = resident_mu(mu);
-    if (dmu != nullptr || !ensure_xsl()) return false;
+    bool ok = dmu == nullptr && ensure_xsl();
+    // With a communicator every rank must take the same branch (a screen and a full pass
+    // issue different all-reduces): the ranks agree once on availability (the digit image
+    // is a per-rank allocation).
+    if (comm) ok = agree_once(screen_agreed_, ok);
+    if (!ok) return false;
     upload_wsl(w, nc);
     d_wsl_ready_ = true;
     double* st_rows = ensure(d_stats, cap_stats, 2 * nc);
@@ -2988,8 +3013,11 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     const int nb = pick_nb(nc);
     const int nfp = 16 * nb;
-    // keep == false, or no room for Y: loss-only pass, completion recomputes the full pass
-    const bool store = keep && ensure_ybuf(nb);
+    // keep == false, or no room for Y: loss-only pass, completion recomputes the full pass.
+    // With a communicator the ranks agree (once) on keeping Y: the two completions issue
+    // different all-reduces.
+    bool store = keep && ensure_ybuf(nb);
+    if (comm && keep) store = agree_once(ybuf_agreed_, store);
     out->nc = nc;
     out->has_h = need_h;
     out->buf.assign(EvalStats::size(nc, need_h), 0.0);

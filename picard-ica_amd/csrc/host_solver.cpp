@@ -213,10 +213,7 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   ev_->want_y2 = !cfg_.ortho && extended_;
   const double t0 = now_ms();
   ev_->eval(wt.data(), nc_, has_mu_ ? mu_.data() : nullptr, cfg_.density, !cfg_.ortho, out);
-  const double dt = now_ms() - t0;
-  eval_ms_ += dt;
-  full_ms_ += dt;
-  ++n_full_ms_;
+  eval_ms_ += now_ms() - t0;
   ++last_evals_;
   ++total_evals_;
 }
@@ -369,6 +366,9 @@ class TransformWorker {
 
 Solver::~Solver() = default;
 
+// screen / full-pass time ratio of the first-try policy (C3 on MI355X: 28 / 83 ms)
+static constexpr double kScreenCostRatio = 0.34;
+
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first,
                                      bool first_loss_only, bool full_first) {  // core.rs:99-150
   // Evaluation schedule: a try is a full fused pass, or a loss-only pass
@@ -466,6 +466,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     // running estimate of p is below 1 − t_s/t_f (measured running means). p is estimated
     // per state of the previous search (accepted at try 1 or not: on C3 the first tries
     // alternate, 0.6 vs 1.0 acceptance), Laplace-smoothed over this fit's first tries.
+    // t_s/t_f: kScreenCostRatio (rank-independent; see below).
     // The gradient fallback (full_first) is accepted at try 1 almost always: full pass.
     // Schedule only: no decision changes.
     bool screen = ortho && !keep_y_ && screen_ok_;
@@ -474,11 +475,12 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       if (full_first) {
         screen = false;
       } else if (first_policy) {
-        const double ts = n_screen_ms_ ? screen_ms_ / n_screen_ms_ : 28.0;
-        const double tf = n_full_ms_ ? full_ms_ / n_full_ms_ : 83.0;
+        // t_s/t_f is a constant (C3: 28 / 83 ms), not the measured means: with one RCCL
+        // communicator every rank must take the same branch (the screen and the full
+        // pass issue different all-reduces), and p_acc is built from decisions alone
         const int st = first_full_ ? 1 : 0;
         const double p_acc = (first_acc_[st] + 1.0) / (first_n_[st] + 2.0);
-        screen = p_acc < 1.0 - ts / tf;
+        screen = p_acc < 1.0 - kScreenCostRatio;
       }
     }
     if (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
@@ -496,10 +498,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       const double t0 = now_ms();
       if (ev_->eval_loss_screen(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(), bnd.data())) {
         screened = true;
-        const double dt = now_ms() - t0;
-        eval_ms_ += dt;
-        screen_ms_ += dt;
-        ++n_screen_ms_;
+        eval_ms_ += now_ms() - t0;
         ++screen_passes_;
         double lo = 0.0, eb = 0.0;
         for (size_t i = 0; i < n; ++i) {

@@ -102,10 +102,8 @@ class Solver {
   uint64_t total_completions_ = 0;
   uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
   bool screen_ok_ = true;  // false once the evaluator declined a screen (then never asked again)
-  // first-try policy: outcomes of descent-direction first tries, running pass times
+  // first-try policy: outcomes of descent-direction first tries
   double first_n_[2] = {0.0, 0.0}, first_acc_[2] = {0.0, 0.0};  // by state: previous search accepted at try 1?
-  double screen_ms_ = 0.0, full_ms_ = 0.0;
-  uint64_t n_screen_ms_ = 0, n_full_ms_ = 0;
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are
