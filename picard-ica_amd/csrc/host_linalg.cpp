@@ -182,8 +182,13 @@ Mat scale(const Mat& a, double s) {
 
 double max_abs(const Mat& a) {
   // fold(0.0, f64::max): NaN entries are skipped by f64::max (core.rs:289)
+  // (f > m ? f : m) is fmax here: m starts at 0 and never becomes NaN, and a NaN f
+  // compares false. Unlike std::fmax it is inlined (no libm call per element).
   double m = 0.0;
-  for (double v : a.a) m = std::fmax(m, std::fabs(v));
+  for (double v : a.a) {
+    const double f = std::fabs(v);
+    m = f > m ? f : m;
+  }
   return m;
 }
 
@@ -437,9 +442,17 @@ Mat matrix_exp(const Mat& a) {
   Mat result = Mat::eye(n), term = Mat::eye(n);
   for (int k = 1; k <= 30; ++k) {
     term = matmul(term, as);
-    for (double& v : term.a) v /= (double)k;
-    for (size_t i = 0; i < result.a.size(); ++i) result.a[i] += term.a[i];
-    if (max_abs(term) < 1e-16) break;
+    // term /= k; result += term; max|term| — one sweep, same per-element operations.
+    const double kd = (double)k;
+    double m = 0.0;
+    for (size_t i = 0; i < term.a.size(); ++i) {
+      const double v = term.a[i] / kd;
+      term.a[i] = v;
+      result.a[i] += v;
+      const double f = std::fabs(v);
+      m = f > m ? f : m;
+    }
+    if (m < 1e-16) break;
   }
   for (int i = 0; i < s; ++i) result = matmul(result, result);
   return result;
