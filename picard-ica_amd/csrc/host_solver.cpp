@@ -7,6 +7,7 @@
 #include "host_solver.hpp"
 #include "host_rng.hpp"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -297,9 +298,12 @@ void Solver::init_core() {  // core.rs:175-209
 // as a newer one arrives. A finished search never waits for it (a stale
 // matrix_exp just completes in the background), which a per-search thread that
 // is joined at the end would do: up to one N³ series per iteration.
+// The helper runs single-threaded: a second OpenMP team beside the driving thread's
+// oversubscribes the host's cores (measured: try 1's map 3.6x slower with half the threads
+// here), and its maps were never waited for (PICARD_TRACE map_wait_ms = 0 at C3 / 8).
 class TransformWorker {
  public:
-  TransformWorker() {
+  TransformWorker() : nthreads_(1) {
     th_ = std::thread([this] { run(); });
   }
   ~TransformWorker() {
@@ -322,15 +326,18 @@ class TransformWorker {
     }
     cv_.notify_all();
   }
-  Mat get(size_t k) {
+  Mat get(size_t k, double* wait_ms) {
+    const double t0 = now_ms();
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] { return ready_[k] != 0; });
+    *wait_ms += now_ms() - t0;
     return out_[k];
   }
 
  private:
+  const int nthreads_;
   void run() {
-    omp_set_num_threads(1);  // background work: leave the cores to the thread driving the device
+    omp_set_num_threads(nthreads_);
     uint64_t done_gen = 0;
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
@@ -392,7 +399,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           ahead_->submit(direction, W_, tries);
         }
       } else {
-        r.w = ahead_->get(k);
+        r.w = ahead_->get(k, &ahead_wait_ms_);
       }
     } else {
       transform = Mat::eye(n);
@@ -553,7 +560,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
 
 bool Solver::step() {
   if (done_) return true;
-  const double step_t0 = now_ms(), eval_t0 = eval_ms_;
+  const double step_t0 = now_ms(), eval_t0 = eval_ms_, wait_t0 = ahead_wait_ms_;
   const size_t n = nc_;
   const double t_f = (double)T_;
   const bool ortho = cfg_.ortho != 0;
@@ -660,9 +667,9 @@ bool Solver::step() {
   if (trace_) {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
-                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f screens %llu rejected %llu\n",
+                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f map_wait_ms %.3f screens %llu rejected %llu\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
-                 res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_,
+                 res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_, ahead_wait_ms_ - wait_t0,
                  (unsigned long long)screen_passes_, (unsigned long long)screen_rejects_);
   }
   prev_step_ = std::move(res.step);

@@ -118,7 +118,8 @@ class Solver {
   // Non-ortho searches evaluate tries >= 2 in one multi-α pass
   // (Evaluator::eval_loss_multi) unless PICARD_NO_MULTI=1.
   bool no_multi_ = false;
-  double eval_ms_ = 0.0, map1_ms_ = 0.0;  // PICARD_TRACE timing: evaluator calls, try-1 map
+  // PICARD_TRACE timing: evaluator calls, try-1 map, waits for the helper's maps
+  double eval_ms_ = 0.0, map1_ms_ = 0.0, ahead_wait_ms_ = 0.0;
   bool trace_ = false;  // PICARD_TRACE=1: one stderr line per iteration (line-search tries)
 };
 
