@@ -189,7 +189,11 @@ int pc_ctx_eval_complete(pc_ctx* ctx, pc_density density, uint32_t flags, double
 int pc_ctx_rowsum(pc_ctx* ctx, double* out /* n_features */, char* err, size_t errlen);
 int pc_ctx_gram(pc_ctx* ctx, const double* mu /* or NULL */, double* out /* nf × nf */,
                 char* err, size_t errlen);
-/* this rank's shard of Y = W·(X−μ) → host (nc × n_local) */
+/* this rank's shard of Y = W·(X−μ) → host (nc × n_local). When the context already holds
+ * the int8 digit image of X at this μ (built by an earlier pass; PC_YSTAGE_F64 not set) and
+ * 64 < nc ≤ 128, nf ≤ 128, Y comes from the exact int8 digit products (fp64-GEMM accuracy,
+ * not the fp64 MFMA store's bits); pc_ctx_sources and pc_ctx_sources_device always agree
+ * bit for bit. No image is built for a sources call alone. */
 int pc_ctx_sources(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, double* out,
                    char* err, size_t errlen);
 /* The same Y kept in HBM for device-side consumers (solver.rs:182,199-214

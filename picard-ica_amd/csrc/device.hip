@@ -2811,6 +2811,26 @@ struct DeviceCtx : Evaluator {
     if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
   }
   uint64_t n_screen_passes_ = 0;
+  // Sources on the int8 digit stage (k_ystore_oz) when this context already holds the digit
+  // image of the current centring: W digits uploaded, blocks b_first … of the image, Y
+  // row-major (ld ldy), samples [0, n_out) of that range. The image is never built for a
+  // transform alone (building it is a pass of its own).
+  bool ystore_oz_ok(size_t nc) const { return xsl_valid_ && oz_shape(nc); }
+  void ystore_oz_run(uint64_t b_first, uint64_t n_out, size_t nc, double* Y, uint64_t ldy) {
+    const uint64_t n_blocks = (n_out + 15) / 16;
+    uint64_t bpw;
+    const int nwg = partition(n_blocks, &bpw);
+    const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
+    static bool attr = false;
+    if (!attr) {
+      HIP_OK(hipFuncSetAttribute((const void*)k_ystore_oz, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr = true;
+    }
+    k_ystore_oz<<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, b_first, bpw, n_blocks, n_out, (int)nc,
+                                                   Y, ldy);
+    HIP_OK(hipGetLastError());
+    ++n_int8_passes_;
+  }
   // Rank agreement on a per-rank capability that selects between branches with different
   // collectives: the first call all-reduces the local flag (all ranks must have it);
   // later calls reuse the answer, and a rank that loses the capability afterwards
@@ -3129,12 +3149,15 @@ struct DeviceCtx : Evaluator {
   void sources(const double* w, size_t nc, const double* mu, double* out) override {
     HIP_OK(hipSetDevice(device));
     resident_mu(mu);  // X is centred in place: Y = W·X
-    ystore_upload(w, nc, nf);
     const uint64_t CH = 1ull << 20;
-    double* Y = ensure(d_chunk, cap_chunk, nc * CH);
+    double* Y = ensure(d_chunk, cap_chunk, nc * CH);  // first: a failed allocation releases the image
+    const bool oz = ystore_oz_ok(nc);
+    if (oz) upload_wsl(w, nc);
+    else ystore_upload(w, nc, nf);
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
       const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
-      ystore_run(X + c0, ldx, nf, nc, cn, Y, CH);
+      if (oz) ystore_oz_run(c0 / 16, cn, nc, Y, CH);
+      else ystore_run(X + c0, ldx, nf, nc, cn, Y, CH);
       HIP_OK(hipMemcpy2DAsync(out + c0, n_local_ * sizeof(double), Y, CH * sizeof(double), cn * sizeof(double), nc,
                               hipMemcpyDeviceToHost, stream));
     }
@@ -3148,12 +3171,15 @@ struct DeviceCtx : Evaluator {
   const double* sources_resident(const double* w, size_t nc, const double* mu, double* kernel_ms) {
     HIP_OK(hipSetDevice(device));
     resident_mu(mu);
-    ystore_upload(w, nc, nf);
-    double* S = ensure(d_src, cap_src, nc * ldx);
+    double* S = ensure(d_src, cap_src, nc * ldx);  // first: a failed allocation releases the image
+    const bool oz = ystore_oz_ok(nc);
+    if (oz) upload_wsl(w, nc);
+    else ystore_upload(w, nc, nf);
     if (ldx > n_local_)  // the padding columns read as zero, like X's
       HIP_OK(hipMemset2DAsync(S + n_local_, ldx * sizeof(double), 0, (ldx - n_local_) * sizeof(double), nc, stream));
     HIP_OK(hipEventRecord(ev[1], stream));
-    ystore_run(X, ldx, nf, nc, n_local_, S, ldx);
+    if (oz) ystore_oz_run(0, n_local_, nc, S, ldx);
+    else ystore_run(X, ldx, nf, nc, n_local_, S, ldx);
     HIP_OK(hipEventRecord(ev[2], stream));
     HIP_OK(hipStreamSynchronize(stream));
     float a = 0;

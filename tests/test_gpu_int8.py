@@ -327,3 +327,40 @@ def test_int8_non_finite_propagates(pa, rng):
         wb[5, 7] = np.inf
         st = ctx.eval(wb, None, d, False)
         assert np.isnan(st["ll"][5]) and np.isfinite(st["ll"][6]), mode
+
+
+@pytest.mark.parametrize("nc,nf,t", [(128, 128, 5003), (100, 128, 20011), (72, 100, 1100003)])
+def test_int8_sources(pa, rng, nc, nf, t):
+    """Sources / transform (solver.rs:182,199-214) on the int8 stage (k_ystore_oz) once the
+    context holds the digit image: against numpy's fp64 W·(X − μ) at 1e-12, against the
+    fp64 MFMA store (k_ystore) at 1e-13; host copy and HBM copy bit-identical, padding zero.
+    t = 1100003 crosses the 2^20-sample chunks of the host-copy path (b_first > 0)."""
+    import ctypes
+    x = laplace_mix(rng, nf, t)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    w = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    ctx.sources(w, mu)  # no digit image yet: the fp64 store, and no image is built for it
+    assert ctx.int8_passes == 0
+    loss_only(ctx, w, mu, pa.DensityType.tanh())  # builds the image
+    n8 = ctx.int8_passes
+    got = ctx.sources(w, mu)
+    assert ctx.int8_passes == n8 + (t + (1 << 20) - 1) // (1 << 20)
+    want = w @ (x - mu[:, None])
+    assert rel_err(got, want) <= TOL, rel_err(got, want)
+    ptr, ld, ms = ctx.sources_device(w, mu)
+    assert ctx.int8_passes == n8 + (t + (1 << 20) - 1) // (1 << 20) + 1
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    dev = np.empty((nc, ld))
+    assert hip.hipMemcpy(dev.ctypes.data, ptr, dev.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    assert np.array_equal(dev[:, :t], got)
+    assert not dev[:, t:].any()
+    ctx.set_y_stage("f64")
+    f64 = ctx.sources(w, mu)
+    assert rel_err(got, f64) <= TOL_MODES, rel_err(got, f64)
+    # per sample: each column against its own fp64 value (the stage's error follows the
+    # sample's scale 2^e_t, not the whole matrix's)
+    col = np.abs(got - f64).max(axis=0) / np.maximum(np.abs(f64).max(axis=0), 1e-300)
+    assert col.max() <= 1e-13, col.max()
