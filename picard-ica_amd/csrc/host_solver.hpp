@@ -17,7 +17,8 @@ std::string rust_e4(double v);  // Rust {:.4e}
 // pass on the device, the cumulant matrices (jade.rs:78-131) and the Jacobi
 // sweeps, then sym_decorrelation(V) (jade.rs:69). Sweep placement:
 // AUTO = host; DEVICE = the cooperative device launch or an error; HOST; AUTO_DEVICE =
-// the device launch where supported, the host otherwise (PICARD_DEVICE_JADE=1).
+// the device launch where supported, the host otherwise. The solver uses AUTO_DEVICE,
+// or AUTO when PICARD_HOST_JADE=1 is set.
 enum JadeSweeps { JADE_SWEEPS_AUTO = 0, JADE_SWEEPS_DEVICE = 1, JADE_SWEEPS_HOST = 2, JADE_SWEEPS_AUTO_DEVICE = 3 };
 struct JadeInfo { size_t sweeps = 0; bool converged = false; bool on_device = false; double moments_s = 0, sweeps_s = 0; };
 size_t jade_max_pairs();  // PICARD_JADE_MAX_PAIRS test hook (SIZE_MAX when unset)
