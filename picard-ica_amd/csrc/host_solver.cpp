@@ -286,6 +286,44 @@ void Solver::init_core() {  // core.rs:175-209
   } else {
     C_ = Mat::eye(n);
   }
+  // whitened covariance for the curvature rejection (orthogonal tanh searches only): used
+  // only when it computes to I within 1e-3, i.e. the whitening is well conditioned
+  if (cfg_.ortho && has_k_ && has_gram_ && cfg_.density.kind == PC_DENSITY_TANH && cfg_.density.alpha > 0.0) {
+    C1_ = matmul_nt(matmul(P_, gram_), P_);
+    for (double& v : C1_.a) v /= (double)T_;
+    double dev = 0.0;
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = 0; j < n; ++j) dev = std::fmax(dev, std::fabs(C1_(i, j) - (i == j ? 1.0 : 0.0)));
+    curv_ok_ = dev < 1e-3;
+  }
+}
+
+// Curvature rejection (schedule only, no decision changes). Along the try path
+// W(α) = expm(αD)·W with D skew-symmetric, y_t(α) = expm(αD)·y_t keeps every ‖y_t‖, and for
+// the tanh density ℓ′ = tanh(a·y) (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a, so the orthogonal loss
+// L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has |L″| ≤ 2a‖D‖₂²·N_eff ≤ a‖D‖_F²·N_eff, with N_eff =
+// Σ_t‖y_t‖²/T = tr(W·C1·Wᵀ) (‖D‖₂² ≤ ‖D‖_F²/2 for skew D). L′(0) = ⟨g, D⟩ = slope.
+// Hence L(α) − L(0) ≥ α·slope − α²·M/2: when that exceeds the rounding of both exact losses
+// (passes and W(α); far above the kernels' 1e-10 relative sum error), the exact pass at α
+// would reject the try (core.rs:127-140) and it need not run. N_eff carries a 2× margin and
+// the slope a lower bound on its own rounding.
+void Solver::set_curvature(const Mat& g, const Mat& d, double slope) {
+  ls_curv_ = 0.0;
+  if (!curv_ok_ || !(slope > 0.0)) return;
+  const size_t n = nc_;
+  const Mat wc = matmul(W_, C1_);
+  double neff = 0.0;
+  for (size_t i = 0; i < n; ++i)
+    for (size_t k = 0; k < n; ++k) neff += wc(i, k) * W_(i, k);
+  neff *= 2.0;
+  double gd = 0.0;
+  for (size_t e = 0; e < g.a.size(); ++e) gd += std::fabs(g.a[e] * d.a[e]);
+  const double a = cfg_.density.alpha;
+  ls_slope_ = slope - 1e-10 * gd;
+  ls_curv_ = a * neff * dot_sum(d, d);
+  // |Σ_i ℓ_i| ≤ Σ|y_i| + N·ln2/a ≤ √(N·N_eff) + N·ln2/a per sample
+  ls_slack_ = 2.0 * (3e-10 * (std::sqrt((double)n * neff) + (double)n * 0.6931471805599453 / a) + 1e-9);
+  if (!std::isfinite(ls_curv_) || !std::isfinite(ls_slope_) || !(ls_slope_ > 0.0)) ls_curv_ = 0.0;
 }
 
 // Orthogonal line search, host side: W_k = expm(α_k·D)·W (core.rs:118-125) for
@@ -467,6 +505,19 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       no_multi_ = true;  // evaluator cannot: per-try passes from now on
     }
     r.tries = k + 1;
+    // Curvature rejection (set_curvature): once the evaluator has shown that it screens (so
+    // the exact-every-try modes keep every pass), a try the bound already rejects needs no pass
+    if (ortho && ls_curv_ > 0.0 && screen_seen_ &&
+        alpha * ls_slope_ - 0.5 * alpha * alpha * ls_curv_ > ls_slack_) {
+      if (k == 0 && !first_loss_only && !full_first) first_n_[first_full_ ? 1 : 0] += 1.0;
+      ++curv_skips_;
+      r.screened_out = true;  // no exact statistics for this W
+      if (trace_)
+        std::fprintf(stderr, "[picard-curv] try %zu alpha %.3e lower bound %.3e reject\n", k + 1, alpha,
+                     alpha * ls_slope_ - 0.5 * alpha * alpha * ls_curv_);
+      alpha /= 2.0;
+      continue;
+    }
     // Orthogonal searches screen their tries when the evaluator has a screen. Try 1 of a
     // descent direction (⟨g, D⟩ < 0) is accepted with some probability p: screening it
     // costs t_s + p·t_f against t_f for a full pass, so it is screened only while the
@@ -505,6 +556,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       const double t0 = now_ms();
       if (ev_->eval_loss_screen(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(), bnd.data())) {
         screened = true;
+        screen_seen_ = true;
         eval_ms_ += now_ms() - t0;
         ++screen_passes_;
         double lo = 0.0, eb = 0.0;
@@ -650,12 +702,14 @@ bool Solver::step() {
   // α and the whole search almost surely fails), where a loss-only pass avoids
   // the wasted G stage. An accepted try is completed either way.
   const double slope = dot_sum(g, direction);
+  set_curvature(g, direction, slope);
   LsResult res = line_search(direction, cfg_.ls_tries, !first_full_, ortho && slope >= 0.0);
   const size_t first_tries = res.tries;
   const bool first_ok = res.success;
   first_full_ = res.success && res.tries == 1;
   if (!res.success) {  // core.rs:349-364
     mem_.clear();
+    ls_curv_ = 0.0;  // the gradient direction descends: nothing to reject by curvature
     res = line_search(scale(g, -1.0), 10, false, false, true);
   }
   if (res.partial) complete(&res.stats);  // the new iterate needs G (H), Σψ′
@@ -667,10 +721,12 @@ bool Solver::step() {
   if (trace_) {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
-                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f map_wait_ms %.3f screens %llu rejected %llu\n",
+                 " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f map_wait_ms %.3f screens %llu rejected %llu"
+                 " curv_skips %llu\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
                  res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_, ahead_wait_ms_ - wait_t0,
-                 (unsigned long long)screen_passes_, (unsigned long long)screen_rejects_);
+                 (unsigned long long)screen_passes_, (unsigned long long)screen_rejects_,
+                 (unsigned long long)curv_skips_);
   }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;

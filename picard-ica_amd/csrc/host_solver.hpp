@@ -103,6 +103,15 @@ class Solver {
   uint64_t total_completions_ = 0;
   uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
   bool screen_ok_ = true;  // false once the evaluator declined a screen (then never asked again)
+  bool screen_seen_ = false;  // a screen has run (the evaluator screens: tries need not all be exact)
+  // Curvature rejection of orthogonal tries (Solver::set_curvature): C1 = P·Gram·Pᵀ/T, the
+  // whitened covariance; per search a lower bound on L'(0), a bound on |L''| along
+  // expm(αD)·W and the rounding slack; ls_curv_ = 0 disables
+  bool curv_ok_ = false;
+  Mat C1_;
+  double ls_slope_ = 0.0, ls_curv_ = 0.0, ls_slack_ = 0.0;
+  uint64_t curv_skips_ = 0;
+  void set_curvature(const Mat& g, const Mat& d, double slope);
   // first-try policy: outcomes of descent-direction first tries
   double first_n_[2] = {0.0, 0.0}, first_acc_[2] = {0.0, 0.0};  // by state: previous search accepted at try 1?
   // Evaluation schedule of a line search (results are bit-identical whatever

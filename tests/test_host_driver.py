@@ -142,3 +142,67 @@ def test_screened_line_search_decisions_unchanged(pa, po, dg, n, t, extended):
     assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
     assert np.array_equal(r1.unmixing, r0.unmixing)
     assert c1["eval"] < c0["eval"]  # rejected tries ran no exact pass
+
+
+def test_curvature_rejection_decisions_unchanged(pa, po, dg, capfd, monkeypatch):
+    """Orthogonal tries rejected by the curvature bound (Solver::set_curvature) run no pass and
+    change no decision: the bench mixture at N=16 has searches along non-descent directions
+    whose small-α tries the bound rejects; the fit is bit-identical to the every-try-exact one."""
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    x, _ = dg.generate_data(16, 20000, 42)[:2]
+
+    def ev(w, mu, d, need_h):
+        return po.pass_stats(w, mu, x, density_of(po, d), need_h)
+
+    def screen(w, mu, d):
+        ll = po.pass_stats(w, mu, x, density_of(po, d), False)["ll"]
+        return ll, 1e-9 * np.abs(ll) + 1e-12
+
+    def fit(with_screen):
+        kw = dict(eval_loss_screen=screen) if with_screen else {}
+        return pa.fit_with_host_evaluator(
+            x.shape[0], x.shape[1], pa.PicardConfig(random_state=42, max_iter=60),
+            rowsum=lambda: x.sum(axis=1), gram=lambda mu: (x - mu[:, None]) @ (x - mu[:, None]).T,
+            eval=ev, sources=lambda w, mu: w @ (x - mu[:, None]), **kw)
+
+    r0 = fit(False)
+    n0 = capfd.readouterr().err.count("[picard-curv]")
+    r1 = fit(True)
+    n1 = capfd.readouterr().err.count("[picard-curv]")
+    assert n0 == 0 and n1 > 0  # only once the evaluator screens
+    assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
+    assert np.array_equal(r1.unmixing, r0.unmixing)
+
+
+@pytest.mark.parametrize("a", [1.0, 0.5, 2.0])
+def test_curvature_bound_holds(a):
+    """The bound behind the curvature rejection: on whitened data, along W(α) = expm(αD)·W with
+    D skew-symmetric, the tanh loss L(α) = Σ_i s_i mean_t ℓ(y_it) satisfies
+    L(α) ≥ L(0) + α·L'(0) − α²·a·‖D‖_F²·N_eff/2, N_eff = mean_t ‖y_t‖², L'(0) = ⟨g, D⟩."""
+    from scipy.linalg import expm
+    rng = np.random.default_rng(5)
+    n, t = 8, 4000
+    x = rng.laplace(size=(n, t))
+    x -= x.mean(axis=1, keepdims=True)
+    ev, u = np.linalg.eigh(x @ x.T / t)
+    x = (u / np.sqrt(ev)).T @ x  # whitened: covariance I
+    w = np.linalg.qr(rng.normal(size=(n, n)))[0]
+    s = np.sign(rng.normal(size=n))
+
+    def ell(y):  # density.rs Tanh log_lik: |y| + log1p(exp(-2a|y|))/a
+        return np.abs(y) + np.log1p(np.exp(-2 * a * np.abs(y))) / a
+
+    def loss(wm):
+        return float(np.sum(s * ell(wm @ x).mean(axis=1)))
+
+    y = w @ x
+    g = s[:, None] * (np.tanh(a * y) @ y.T) / t
+    neff = float(np.mean(np.sum(y * y, axis=0)))
+    for _ in range(20):
+        d = rng.normal(size=(n, n)) * rng.uniform(0.01, 1.0)
+        d = (d - d.T) / 2
+        slope = float(np.sum(g * d))
+        m = a * neff * float(np.sum(d * d))
+        for alpha in 2.0 ** -np.arange(0, 10):
+            lhs = loss(expm(alpha * d) @ w) - loss(w)
+            assert lhs >= alpha * slope - alpha * alpha * m / 2 - 1e-12, (alpha, lhs, slope, m)
