@@ -299,28 +299,33 @@ void Solver::init_core() {  // core.rs:175-209
 }
 
 // Curvature rejection (schedule only, no decision changes). Along the try path
-// W(α) = expm(αD)·W with D skew-symmetric, y_t(α) = expm(αD)·y_t keeps every ‖y_t‖, and for
-// the tanh density ℓ′ = tanh(a·y) (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a, so the orthogonal loss
-// L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has |L″| ≤ 2a‖D‖₂²·N_eff ≤ a‖D‖_F²·N_eff, with N_eff =
-// Σ_t‖y_t‖²/T = tr(W·C1·Wᵀ) (‖D‖₂² ≤ ‖D‖_F²/2 for skew D). L′(0) = ⟨g, D⟩ = slope.
-// Hence L(α) − L(0) ≥ α·slope − α²·M/2: when that exceeds the rounding of both exact losses
-// (passes and W(α); far above the kernels' 1e-10 relative sum error), the exact pass at α
-// would reject the try (core.rs:127-140) and it need not run. N_eff carries a 2× margin and
-// the slope a lower bound on its own rounding.
+// W(α) = expm(αD)·W, y_t(α) = E·y_t with E = expm(αD) orthogonal and commuting with D (D
+// skew-symmetric), so with Cy = Σ_t y_t y_tᵀ/T = W·C1·Wᵀ the sums Σ_t‖y_t‖²/T = tr(Cy) = N_eff,
+// Σ_t‖D y_t‖²/T = tr(D·Cy·Dᵀ) and Σ_t‖D² y_t‖²/T = tr(D²·Cy·D²ᵀ) do not depend on α. For the
+// tanh density ℓ′ = tanh(a·y) (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a, so the orthogonal loss
+// L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has
+//   |L″| = |Σ_t Σ_i s_i (ℓ″(y_it)(D y_t)_i² + ℓ′(y_it)(D² y_t)_i)|/T
+//        ≤ a·tr(D·Cy·Dᵀ) + a·√(N_eff · tr(D²·Cy·D²ᵀ))   (Cauchy–Schwarz over t) = M,
+// and L′(0) = ⟨g, D⟩ = slope. Hence L(α) − L(0) ≥ α·slope − α²·M/2: when that exceeds the
+// rounding of both exact losses (passes and W(α); far above the kernels' 1e-10 relative sum
+// error), the exact pass at α would reject the try (core.rs:127-140) and it need not run.
+// Cy carries a 2× margin and the slope a lower bound on its own rounding.
 void Solver::set_curvature(const Mat& g, const Mat& d, double slope) {
   ls_curv_ = 0.0;
   if (!curv_ok_ || !(slope > 0.0)) return;
   const size_t n = nc_;
-  const Mat wc = matmul(W_, C1_);
+  Mat cy = matmul_nt(matmul(W_, C1_), W_);
+  for (double& v : cy.a) v *= 2.0;
   double neff = 0.0;
-  for (size_t i = 0; i < n; ++i)
-    for (size_t k = 0; k < n; ++k) neff += wc(i, k) * W_(i, k);
-  neff *= 2.0;
+  for (size_t i = 0; i < n; ++i) neff += cy(i, i);
+  const Mat d2 = matmul(d, d);
+  const double a1 = dot_sum(matmul(d, cy), d);    // tr(D·Cy·Dᵀ) = Σ (D·Cy)∘D
+  const double a2 = dot_sum(matmul(d2, cy), d2);  // tr(D²·Cy·D²ᵀ)
   double gd = 0.0;
   for (size_t e = 0; e < g.a.size(); ++e) gd += std::fabs(g.a[e] * d.a[e]);
   const double a = cfg_.density.alpha;
   ls_slope_ = slope - 1e-10 * gd;
-  ls_curv_ = a * neff * dot_sum(d, d);
+  ls_curv_ = a * (std::fabs(a1) + std::sqrt(std::fabs(neff * a2)));
   // |Σ_i ℓ_i| ≤ Σ|y_i| + N·ln2/a ≤ √(N·N_eff) + N·ln2/a per sample
   ls_slack_ = 2.0 * (3e-10 * (std::sqrt((double)n * neff) + (double)n * 0.6931471805599453 / a) + 1e-9);
   if (!std::isfinite(ls_curv_) || !std::isfinite(ls_slope_) || !(ls_slope_ > 0.0)) ls_curv_ = 0.0;

@@ -178,7 +178,8 @@ def test_curvature_rejection_decisions_unchanged(pa, po, dg, capfd, monkeypatch)
 def test_curvature_bound_holds(a):
     """The bound behind the curvature rejection: on whitened data, along W(α) = expm(αD)·W with
     D skew-symmetric, the tanh loss L(α) = Σ_i s_i mean_t ℓ(y_it) satisfies
-    L(α) ≥ L(0) + α·L'(0) − α²·a·‖D‖_F²·N_eff/2, N_eff = mean_t ‖y_t‖², L'(0) = ⟨g, D⟩."""
+    L(α) ≥ L(0) + α·L'(0) − α²·M/2 with M = a·(tr(D·Cy·Dᵀ) + √(N_eff·tr(D²·Cy·D²ᵀ))),
+    Cy = mean_t y_t y_tᵀ, N_eff = tr(Cy), L'(0) = ⟨g, D⟩ (no margin here: the solver doubles Cy)."""
     from scipy.linalg import expm
     rng = np.random.default_rng(5)
     n, t = 8, 4000
@@ -197,12 +198,14 @@ def test_curvature_bound_holds(a):
 
     y = w @ x
     g = s[:, None] * (np.tanh(a * y) @ y.T) / t
-    neff = float(np.mean(np.sum(y * y, axis=0)))
+    cy = y @ y.T / t
+    neff = float(np.trace(cy))
     for _ in range(20):
         d = rng.normal(size=(n, n)) * rng.uniform(0.01, 1.0)
         d = (d - d.T) / 2
         slope = float(np.sum(g * d))
-        m = a * neff * float(np.sum(d * d))
+        d2 = d @ d
+        m = a * (np.trace(d @ cy @ d.T) + np.sqrt(neff * np.trace(d2 @ cy @ d2.T)))
         for alpha in 2.0 ** -np.arange(0, 10):
             lhs = loss(expm(alpha * d) @ w) - loss(w)
             assert lhs >= alpha * slope - alpha * alpha * m / 2 - 1e-12, (alpha, lhs, slope, m)
