@@ -300,35 +300,59 @@ void Solver::init_core() {  // core.rs:175-209
 
 // Curvature rejection (schedule only, no decision changes). Along the try path
 // W(α) = expm(αD)·W, y_t(α) = E·y_t with E = expm(αD) orthogonal and commuting with D (D
-// skew-symmetric), so with Cy = Σ_t y_t y_tᵀ/T = W·C1·Wᵀ the sums Σ_t‖y_t‖²/T = tr(Cy) = N_eff,
-// Σ_t‖D y_t‖²/T = tr(D·Cy·Dᵀ) and Σ_t‖D² y_t‖²/T = tr(D²·Cy·D²ᵀ) do not depend on α. For the
-// tanh density ℓ′ = tanh(a·y) (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a, so the orthogonal loss
-// L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has
-//   |L″| = |Σ_t Σ_i s_i (ℓ″(y_it)(D y_t)_i² + ℓ′(y_it)(D² y_t)_i)|/T
-//        ≤ a·tr(D·Cy·Dᵀ) + a·√(N_eff · tr(D²·Cy·D²ᵀ))   (Cauchy–Schwarz over t) = M,
-// and L′(0) = ⟨g, D⟩ = slope. Hence L(α) − L(0) ≥ α·slope − α²·M/2: when that exceeds the
-// rounding of both exact losses (passes and W(α); far above the kernels' 1e-10 relative sum
-// error), the exact pass at α would reject the try (core.rs:127-140) and it need not run.
-// Cy carries a 2× margin and the slope a lower bound on its own rounding.
-void Solver::set_curvature(const Mat& g, const Mat& d, double slope) {
+// skew-symmetric), so with Cy = Σ_t y_t y_tᵀ/T = W·C1·Wᵀ the sums A_k = Σ_t‖D^k y_t‖²/T =
+// tr(D^k·Cy·D^kᵀ) (A_0 = N_eff) do not depend on α. For the tanh density ℓ′ = tanh(a·y)
+// (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a. The orthogonal loss L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has
+// L′(0) = ⟨g, D⟩ = slope and L″ = u + v with
+//   u(α) = Σ_t Σ_i s_i ℓ″(y_it)(D y_t)_i² / T   ≥ 0 if every s_i = +1, else ≥ −a·A_1;
+//   v(α) = Σ_t Σ_i s_i ℓ′(y_it)(D² y_t)_i / T,  v(0) = ⟨g_s, D²⟩ (g_s = s_i·G_ij/T, the
+//          signed gradient before the skew part), |v′| ≤ a·√(A_1·A_2) + a·√(A_0·A_3) = K_3,
+//   |u|, |v| ≤ a·A_1, a·√(A_0·A_2)   (Cauchy–Schwarz over t).
+// Two lower bounds on L(α) − L(0) follow, and the larger is used:
+//   α·slope − α²·M/2, M = a·A_1 + a·√(A_0·A_2);
+//   α·slope + α²·(v(0) − [some s_i < 0]·a·A_1)/2 − α³·K_3/6.
+// When it exceeds the rounding of both exact losses (passes and W(α); far above the kernels'
+// 1e-10 relative sum error), the exact pass at α would reject the try (core.rs:127-140), so it
+// need not run. Cy carries a 2× margin; slope and v(0) are lowered by their rounding bounds.
+void Solver::set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slope) {
   ls_curv_ = 0.0;
   if (!curv_ok_ || !(slope > 0.0)) return;
   const size_t n = nc_;
+  bool any_neg = false;
+  for (size_t i = 0; i < n; ++i) {
+    if (!(signs_[i] == 1.0 || signs_[i] == -1.0)) return;
+    any_neg |= signs_[i] < 0.0;
+  }
   Mat cy = matmul_nt(matmul(W_, C1_), W_);
   for (double& v : cy.a) v *= 2.0;
-  double neff = 0.0;
-  for (size_t i = 0; i < n; ++i) neff += cy(i, i);
-  const Mat d2 = matmul(d, d);
-  const double a1 = dot_sum(matmul(d, cy), d);    // tr(D·Cy·Dᵀ) = Σ (D·Cy)∘D
-  const double a2 = dot_sum(matmul(d2, cy), d2);  // tr(D²·Cy·D²ᵀ)
-  double gd = 0.0;
+  double a0 = 0.0;
+  for (size_t i = 0; i < n; ++i) a0 += cy(i, i);
+  const Mat d2 = matmul(d, d), d3 = matmul(d2, d);
+  const double a1 = std::fabs(dot_sum(matmul(d, cy), d));    // tr(D·Cy·Dᵀ) = Σ (D·Cy)∘D
+  const double a2 = std::fabs(dot_sum(matmul(d2, cy), d2));  // tr(D²·Cy·D²ᵀ)
+  const double a3 = std::fabs(dot_sum(matmul(d3, cy), d3));  // tr(D³·Cy·D³ᵀ)
+  double gd = 0.0, gd2 = 0.0, v0 = 0.0;
   for (size_t e = 0; e < g.a.size(); ++e) gd += std::fabs(g.a[e] * d.a[e]);
+  for (size_t e = 0; e < gs.a.size(); ++e) {
+    v0 += gs.a[e] * d2.a[e];
+    gd2 += std::fabs(gs.a[e] * d2.a[e]);
+  }
   const double a = cfg_.density.alpha;
   ls_slope_ = slope - 1e-10 * gd;
-  ls_curv_ = a * (std::fabs(a1) + std::sqrt(std::fabs(neff * a2)));
+  ls_curv_ = a * (a1 + std::sqrt(a0 * a2));
+  ls_q_ = v0 - 1e-10 * gd2 - (any_neg ? a * a1 : 0.0);
+  ls_k3_ = a * (std::sqrt(a1 * a2) + std::sqrt(a0 * a3));
   // |Σ_i ℓ_i| ≤ Σ|y_i| + N·ln2/a ≤ √(N·N_eff) + N·ln2/a per sample
-  ls_slack_ = 2.0 * (3e-10 * (std::sqrt((double)n * neff) + (double)n * 0.6931471805599453 / a) + 1e-9);
-  if (!std::isfinite(ls_curv_) || !std::isfinite(ls_slope_) || !(ls_slope_ > 0.0)) ls_curv_ = 0.0;
+  ls_slack_ = 2.0 * (3e-10 * (std::sqrt((double)n * a0) + (double)n * 0.6931471805599453 / a) + 1e-9);
+  if (!std::isfinite(ls_curv_) || !std::isfinite(ls_slope_) || !std::isfinite(ls_q_) || !std::isfinite(ls_k3_) ||
+      !(ls_slope_ > 0.0))
+    ls_curv_ = 0.0;
+}
+
+double Solver::curvature_lower_bound(double alpha) const {
+  const double b2 = alpha * ls_slope_ - 0.5 * alpha * alpha * ls_curv_;
+  const double b3 = alpha * ls_slope_ + 0.5 * alpha * alpha * ls_q_ - alpha * alpha * alpha * ls_k3_ / 6.0;
+  return std::fmax(b2, b3);
 }
 
 // Orthogonal line search, host side: W_k = expm(α_k·D)·W (core.rs:118-125) for
@@ -512,14 +536,13 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     r.tries = k + 1;
     // Curvature rejection (set_curvature): once the evaluator has shown that it screens (so
     // the exact-every-try modes keep every pass), a try the bound already rejects needs no pass
-    if (ortho && ls_curv_ > 0.0 && screen_seen_ &&
-        alpha * ls_slope_ - 0.5 * alpha * alpha * ls_curv_ > ls_slack_) {
+    if (ortho && ls_curv_ > 0.0 && screen_seen_ && curvature_lower_bound(alpha) > ls_slack_) {
       if (k == 0 && !first_loss_only && !full_first) first_n_[first_full_ ? 1 : 0] += 1.0;
       ++curv_skips_;
       r.screened_out = true;  // no exact statistics for this W
       if (trace_)
         std::fprintf(stderr, "[picard-curv] try %zu alpha %.3e lower bound %.3e reject\n", k + 1, alpha,
-                     alpha * ls_slope_ - 0.5 * alpha * alpha * ls_curv_);
+                     curvature_lower_bound(alpha));
       alpha /= 2.0;
       continue;
     }
@@ -664,6 +687,7 @@ bool Solver::step() {
       }
     regularize_hessian(h, h_off, cfg_.lambda_min);
   }
+  const Mat gs = g;  // signed gradient before the skew part (curvature rejection)
   if (ortho) {  // core.rs:280-286
     g = skew_symmetric(g);
   } else {
@@ -707,7 +731,7 @@ bool Solver::step() {
   // α and the whole search almost surely fails), where a loss-only pass avoids
   // the wasted G stage. An accepted try is completed either way.
   const double slope = dot_sum(g, direction);
-  set_curvature(g, direction, slope);
+  set_curvature(g, gs, direction, slope);
   LsResult res = line_search(direction, cfg_.ls_tries, !first_full_, ortho && slope >= 0.0);
   const size_t first_tries = res.tries;
   const bool first_ok = res.success;

@@ -109,9 +109,10 @@ class Solver {
   // expm(αD)·W and the rounding slack; ls_curv_ = 0 disables
   bool curv_ok_ = false;
   Mat C1_;
-  double ls_slope_ = 0.0, ls_curv_ = 0.0, ls_slack_ = 0.0;
+  double ls_slope_ = 0.0, ls_curv_ = 0.0, ls_q_ = 0.0, ls_k3_ = 0.0, ls_slack_ = 0.0;
   uint64_t curv_skips_ = 0;
-  void set_curvature(const Mat& g, const Mat& d, double slope);
+  void set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slope);
+  double curvature_lower_bound(double alpha) const;
   // first-try policy: outcomes of descent-direction first tries
   double first_n_[2] = {0.0, 0.0}, first_acc_[2] = {0.0, 0.0};  // by state: previous search accepted at try 1?
   // Evaluation schedule of a line search (results are bit-identical whatever

@@ -174,12 +174,14 @@ def test_curvature_rejection_decisions_unchanged(pa, po, dg, capfd, monkeypatch)
     assert np.array_equal(r1.unmixing, r0.unmixing)
 
 
-@pytest.mark.parametrize("a", [1.0, 0.5, 2.0])
-def test_curvature_bound_holds(a):
-    """The bound behind the curvature rejection: on whitened data, along W(α) = expm(αD)·W with
-    D skew-symmetric, the tanh loss L(α) = Σ_i s_i mean_t ℓ(y_it) satisfies
-    L(α) ≥ L(0) + α·L'(0) − α²·M/2 with M = a·(tr(D·Cy·Dᵀ) + √(N_eff·tr(D²·Cy·D²ᵀ))),
-    Cy = mean_t y_t y_tᵀ, N_eff = tr(Cy), L'(0) = ⟨g, D⟩ (no margin here: the solver doubles Cy)."""
+@pytest.mark.parametrize("a,mixed", [(1.0, True), (1.0, False), (0.5, True), (2.0, False)])
+def test_curvature_bound_holds(a, mixed):
+    """The bounds behind the curvature rejection (Solver::set_curvature): on whitened data,
+    along W(α) = expm(αD)·W with D skew-symmetric, the tanh loss L(α) = Σ_i s_i mean_t ℓ(y_it)
+    satisfies L(α) − L(0) ≥ max(α·s − α²·M/2, α·s + α²·(v0 − [s_i < 0 somewhere]·a·A1)/2 −
+    α³·K3/6) with A_k = tr(D^k·Cy·D^kᵀ), Cy = mean_t y_t y_tᵀ, M = a·(A1 + √(A0·A2)),
+    K3 = a·(√(A1·A2) + √(A0·A3)), v0 = ⟨g_s, D²⟩ (g_s = s_i·(ψ·Yᵀ)_ij/T), s = ⟨g_s, D⟩
+    (no margins here: the solver doubles Cy)."""
     from scipy.linalg import expm
     rng = np.random.default_rng(5)
     n, t = 8, 4000
@@ -188,7 +190,7 @@ def test_curvature_bound_holds(a):
     ev, u = np.linalg.eigh(x @ x.T / t)
     x = (u / np.sqrt(ev)).T @ x  # whitened: covariance I
     w = np.linalg.qr(rng.normal(size=(n, n)))[0]
-    s = np.sign(rng.normal(size=n))
+    s = np.sign(rng.normal(size=n)) if mixed else np.ones(n)
 
     def ell(y):  # density.rs Tanh log_lik: |y| + log1p(exp(-2a|y|))/a
         return np.abs(y) + np.log1p(np.exp(-2 * a * np.abs(y))) / a
@@ -197,15 +199,20 @@ def test_curvature_bound_holds(a):
         return float(np.sum(s * ell(wm @ x).mean(axis=1)))
 
     y = w @ x
-    g = s[:, None] * (np.tanh(a * y) @ y.T) / t
+    gs = s[:, None] * (np.tanh(a * y) @ y.T) / t
     cy = y @ y.T / t
-    neff = float(np.trace(cy))
+    tr = lambda m: float(np.trace(m @ cy @ m.T))  # noqa: E731
     for _ in range(20):
         d = rng.normal(size=(n, n)) * rng.uniform(0.01, 1.0)
         d = (d - d.T) / 2
-        slope = float(np.sum(g * d))
+        slope = float(np.sum(gs * d))
         d2 = d @ d
-        m = a * (np.trace(d @ cy @ d.T) + np.sqrt(neff * np.trace(d2 @ cy @ d2.T)))
+        a0, a1, a2, a3 = float(np.trace(cy)), tr(d), tr(d2), tr(d2 @ d)
+        m = a * (a1 + np.sqrt(a0 * a2))
+        q = float(np.sum(gs * d2)) - (a * a1 if np.any(s < 0) else 0.0)
+        k3 = a * (np.sqrt(a1 * a2) + np.sqrt(a0 * a3))
         for alpha in 2.0 ** -np.arange(0, 10):
             lhs = loss(expm(alpha * d) @ w) - loss(w)
-            assert lhs >= alpha * slope - alpha * alpha * m / 2 - 1e-12, (alpha, lhs, slope, m)
+            b2 = alpha * slope - alpha * alpha * m / 2
+            b3 = alpha * slope + alpha * alpha * q / 2 - alpha ** 3 * k3 / 6
+            assert lhs >= max(b2, b3) - 1e-12, (alpha, lhs, b2, b3)
