@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "evaluator.hpp"
+#include "host_linalg.hpp"
 
 namespace pcamd {
 size_t jade_max_pairs();  // host_solver.cpp (PICARD_JADE_MAX_PAIRS test hook)
@@ -2019,6 +2020,30 @@ struct DeviceCtx : Evaluator {
   double last_kernel_ms = 0, last_call_ms = 0;
   double sum_kernel_ms = 0, sum_call_ms = 0;
   uint64_t n_kernel = 0;
+  // Pinned host staging for the per-pass uploads (W image, W digit image): the copy is
+  // issued asynchronously and an event after it guards the slot — the next writer of the
+  // slot waits on that event, so no stream synchronisation follows the upload.
+  struct PinSlot { void* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
+  PinSlot pin_w_, pin_wsl_;
+  void* pin_acquire(PinSlot& sl, size_t bytes) {
+    if (sl.pending) {
+      HIP_OK(hipEventSynchronize(sl.ev));
+      sl.pending = false;
+    }
+    if (sl.cap < bytes) {
+      if (sl.p) HIP_OK(hipHostFree(sl.p));
+      sl.p = nullptr;
+      sl.cap = 0;
+      HIP_OK(hipHostMalloc(&sl.p, bytes, 0));
+      sl.cap = bytes;
+    }
+    if (!sl.ev) HIP_OK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    return sl.p;
+  }
+  void pin_release(PinSlot& sl) {  // after the copies from the slot are enqueued
+    HIP_OK(hipEventRecord(sl.ev, stream));
+    sl.pending = true;
+  }
 
   DeviceCtx(int dev, int rk, int ws, const char* uid) : device(dev), rank(rk), world(ws) {
     HIP_OK(hipSetDevice(device));
@@ -2043,6 +2068,11 @@ struct DeviceCtx : Evaluator {
     for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsl, (void*)d_wsc})
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (PinSlot* sl : {&pin_w_, &pin_wsl_}) {
+      if (sl->pending) (void)hipEventSynchronize(sl->ev);
+      if (sl->p) (void)hipHostFree(sl->p);
+      if (sl->ev) (void)hipEventDestroy(sl->ev);
+    }
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -2361,11 +2391,14 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipEventRecord(ev[2], stream));
     } else if (fused) {
       const int ncp = 16 * nb;
-      std::vector<double> wp((size_t)ncp * nfp, 0.0);
+      const size_t nwp = (size_t)ncp * nfp;
+      ensure(d_w, cap_w, nwp);
+      double* wp = (double*)pin_acquire(pin_w_, nwp * sizeof(double));
+      std::fill(wp, wp + nwp, 0.0);
       for (size_t i = 0; i < nc; ++i)
         for (size_t k = 0; k < nf; ++k) wp[i * nfp + k] = w[i * nf + k];
-      ensure(d_w, cap_w, wp.size());
-      HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+      HIP_OK(hipMemcpyAsync(d_w, wp, nwp * sizeof(double), hipMemcpyHostToDevice, stream));
+      pin_release(pin_w_);
       oz_fused_ready_ = false;
       if (dmu == nullptr && !need_h && dens != DENS_LINEAR && oz_shape(nc) && ensure_xsl()) {
         upload_wsl(w, nc);
@@ -2739,52 +2772,20 @@ struct DeviceCtx : Evaluator {
     if (wsl_nc_ == nc && wsl_w_.size() == nc * nf && std::memcmp(wsl_w_.data(), w, nc * nf * sizeof(double)) == 0)
       return;
     constexpr size_t IMG = (size_t)8 * OZ_SLICES * 2 * 64 * 16;
-    std::vector<uint8_t> img(IMG, 0);
-    std::vector<double> sc(128, 0x1p-12);
-    constexpr double SH = 0x1.8p52;
-    for (size_t i = 0; i < nc; ++i) {
-      double mx = 0.0;
-      bool bad = false;  // a NaN / ±inf weight: the row's scale becomes NaN (y = NaN, as in fp64)
-      for (size_t k = 0; k < nf; ++k) {
-        bad |= !std::isfinite(w[i * nf + k]);
-        mx = std::fmax(mx, std::fabs(w[i * nf + k]));
-      }
-      if (bad) {
-        sc[i] = std::nan("");
-        continue;  // zero digits
-      }
-      int e = 0;
-      if (mx > 0.0) (void)std::frexp(mx, &e);
-      sc[i] = std::ldexp(1.0, e - 12);
-      const bool tiny = 6 - e > 1000;  // a row of subnormal size: 2^(6 − e) would overflow
-      const double s6 = tiny ? 0.0 : std::ldexp(1.0, 6 - e);
-      const size_t wave = i >> 4, n = i & 15;
-      for (size_t k = 0; k < nf; ++k) {
-        double v = tiny ? std::ldexp(w[i * nf + k], 6 - e) : w[i * nf + k] * s6;
-        int dg[OZ_SLICES];
-        for (int a = 0; a < OZ_SLICES; ++a) {
-          const double r = (v + SH) - SH;
-          dg[a] = (int)r;
-          v = (v - r) * 256.0;
-        }
-        for (int a = OZ_SLICES - 1; a > 0; --a) {
-          if (dg[a] > 127) { dg[a] -= 256; dg[a - 1] += 1; }
-          else if (dg[a] < -128) { dg[a] += 256; dg[a - 1] -= 1; }
-        }
-        const size_t s = k >> 6, lane = n + 16 * ((k >> 4) & 3), j = k & 15;
-        for (int a = 0; a < OZ_SLICES; ++a)
-          img[(((wave * OZ_SLICES + a) * 2 + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
-      }
-    }
-    wsl_w_.assign(w, w + nc * nf);
-    wsl_nc_ = nc;
     if (!d_wsl) {
       HIP_OK(hipMalloc(&d_wsl, IMG));
       HIP_OK(hipMalloc(&d_wsc, 128 * sizeof(double)));
     }
-    HIP_OK(hipMemcpyAsync(d_wsl, img.data(), IMG, hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(d_wsc, sc.data(), 128 * sizeof(double), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipStreamSynchronize(stream));  // the host images must outlive the copies
+    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, IMG + 128 * sizeof(double));
+    double* sc = (double*)(img + IMG);
+    std::memset(img, 0, IMG);
+    for (int i = 0; i < 128; ++i) sc[i] = 0x1p-12;
+    oz_split_rows(w, nc, nf, img, sc);  // host_linalg.cpp: rows split over the host threads
+    wsl_w_.assign(w, w + nc * nf);
+    wsl_nc_ = nc;
+    HIP_OK(hipMemcpyAsync(d_wsl, img, IMG, hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsc, sc, 128 * sizeof(double), hipMemcpyHostToDevice, stream));
+    pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
   template <int D, bool Q, int DMAX = OZ_SLICES - 1>
   void launch_loss_oz(double alpha, bool store, double* st_rows) {
@@ -2895,7 +2896,10 @@ struct DeviceCtx : Evaluator {
     std::vector<double> bnd(nc);
     for (size_t i = 0; i < nc; ++i) {
       double mx = 0.0;
-      for (size_t k = 0; k < nf; ++k) mx = std::fmax(mx, std::fabs(w[i * nf + k]));
+      for (size_t k = 0; k < nf; ++k) {
+        const double f = std::fabs(w[i * nf + k]);
+        mx = f > mx ? f : mx;  // = fmax: a NaN weight is skipped, as fmax skips it
+      }
       int e = 0;
       if (mx > 0.0) (void)std::frexp(mx, &e);
       bnd[i] = std::ldexp(tail, e - 12) * (1.0 + 1e-12);

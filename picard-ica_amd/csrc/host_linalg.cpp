@@ -527,4 +527,52 @@ bool invert_matrix(const Mat& m, Mat* out) {
   return true;
 }
 
+// W's radix-256 digits for the int8 Y stage (DeviceCtx::upload_wsl, ozaki.inc "Layout"): per
+// row i, scale sc[i] = 2^(f_i − 12) with max_k |w_ik| < 2^f_i, and 7 signed digits per weight
+// of 64·w·2^-f_i by a shifter rint (exact for |v| < 2^51), ±128/±129 folded into the digit
+// above; img[wave][digit][kstep][lane][16 B] as the i8 MFMA B operand. A NaN / ±inf weight
+// makes the row's scale NaN (zero digits), as the fp64 stage would give NaN.
+void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc) {
+  constexpr double SH = 0x1.8p52;
+  constexpr int OZ_SLICES = 7;
+  // rows are independent (each writes its own digit bytes and scale): split over the threads
+#pragma omp parallel for schedule(static) if (nc * nf >= 4096)
+  for (long ii = 0; ii < (long)nc; ++ii) {
+    const size_t i = (size_t)ii;
+    double mx = 0.0;
+    bool bad = false;  // a NaN / ±inf weight: the row's scale becomes NaN (y = NaN, as in fp64)
+    for (size_t k = 0; k < nf; ++k) {
+      const double f = std::fabs(w[i * nf + k]);
+      bad |= !std::isfinite(w[i * nf + k]);
+      mx = f > mx ? f : mx;  // = fmax (NaN rows are flagged by bad), without a libm call
+    }
+    if (bad) {
+      sc[i] = std::nan("");
+      continue;  // zero digits
+    }
+    int e = 0;
+    if (mx > 0.0) (void)std::frexp(mx, &e);
+    sc[i] = std::ldexp(1.0, e - 12);
+    const bool tiny = 6 - e > 1000;  // a row of subnormal size: 2^(6 − e) would overflow
+    const double s6 = tiny ? 0.0 : std::ldexp(1.0, 6 - e);
+    const size_t wave = i >> 4, n = i & 15;
+    for (size_t k = 0; k < nf; ++k) {
+      double v = tiny ? std::ldexp(w[i * nf + k], 6 - e) : w[i * nf + k] * s6;
+      int dg[OZ_SLICES];
+      for (int a = 0; a < OZ_SLICES; ++a) {
+        const double r = (v + SH) - SH;
+        dg[a] = (int)r;
+        v = (v - r) * 256.0;
+      }
+      for (int a = OZ_SLICES - 1; a > 0; --a) {
+        if (dg[a] > 127) { dg[a] -= 256; dg[a - 1] += 1; }
+        else if (dg[a] < -128) { dg[a] += 256; dg[a - 1] -= 1; }
+      }
+      const size_t s = k >> 6, lane = n + 16 * ((k >> 4) & 3), j = k & 15;
+      for (int a = 0; a < OZ_SLICES; ++a)
+        img[(((wave * OZ_SLICES + a) * 2 + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
+    }
+  }
+}
+
 }  // namespace pcamd

@@ -3,6 +3,7 @@
 // ndarray-linalg 0.18 (eigh → Jacobi, sln_det → partially pivoted LU).
 #pragma once
 #include <cstddef>
+#include <cstdint>
 #include <vector>
 
 namespace pcamd {
@@ -31,6 +32,8 @@ Mat add(const Mat& a, const Mat& b);
 Mat sub(const Mat& a, const Mat& b);
 Mat scale(const Mat& a, double s);
 double max_abs(const Mat& a);
+// int8 digit image of W rows for the device Y stage (host_linalg.cpp)
+void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc);
 double dot_sum(const Mat& a, const Mat& b);       // Σ a∘b
 
 // Symmetric eigendecomposition (cyclic Jacobi). Eigenvalues ascending (as
