@@ -45,6 +45,13 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header. 2: pc_host_evaluator grew the eval_loss_multi and
+ * eval_loss_screen slots (a caller built against revision 1 must be rebuilt), the
+ * rank-group entry points (pc_group_*, pc_ctx_create_in_group, pc_ctx_comm_stats,
+ * pc_ctx_abort) and pc_ctx_release_caches were added. pc_abi_version() returns the
+ * revision the library was built with. */
+#define PC_ABI_VERSION 2
+
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {
   PC_OK = 0,
@@ -117,6 +124,7 @@ double pc_amari_distance(const double* w, const double* a, uint64_t n);
 void pc_permute(const double* a, uint64_t n, int32_t scale, double* out);
 const char* pc_error_name(int status);
 const char* pc_version(void);
+int pc_abi_version(void);
 
 /* ---- device context: X resident in HBM, optionally T-sharded over ranks --- */
 typedef struct pc_ctx pc_ctx;
@@ -137,6 +145,38 @@ int pc_rccl_unique_id(char id_out[128]);
 int pc_ctx_create(int32_t device, int32_t rank, int32_t world_size, const char* rccl_id /* or NULL */,
                   pc_ctx** out, char* err, size_t errlen);
 void pc_ctx_destroy(pc_ctx* ctx);
+
+/* In-process rank group: world_size contexts in ONE process, each driven by its own host
+ * thread (they may share one GPU), exchange every pass's statistics through host memory —
+ * a fixed rank-order sum, identical bits on every rank — instead of RCCL. It runs the
+ * communicator code path of the one-process-per-GPU run (rank-replicated solvers, the
+ * per-pass all-reduce, the capability agreements) on a single device. Every all-reduce
+ * also checks that all ranks issued the same collective (call site and length) and
+ * fails the group if they diverged. The group is reference-counted: destroying it while
+ * contexts still use it is allowed. */
+typedef struct pc_group pc_group;
+int pc_group_create_local(int32_t world_size, pc_group** out, char* err, size_t errlen);
+void pc_group_destroy(pc_group* g);
+int pc_ctx_create_in_group(int32_t device, int32_t rank, pc_group* g, pc_ctx** out, char* err, size_t errlen);
+/* Communicator state of a context: [0] all-reduces issued, [1] capability agreements
+ * asked (int8 digit image / kept Y, DeviceCtx::agree_once), [2] the screen agreement,
+ * [3] the kept-Y agreement (0 not asked, 1 every rank has it, -1 not every rank),
+ * [4] 1 once the group was aborted, [5] world size, [6] 1 RCCL, 2 in-process group,
+ * 0 none. */
+void pc_ctx_comm_stats(const pc_ctx* ctx, int64_t out[7]);
+/* Abort the context's rank group: every rank's pending and later collectives (RCCL:
+ * through ncclCommAbort and a shared abort word the peers poll while they wait) end
+ * with PC_ERR_COMPUTATION. Any pc_ctx_* / pc_solver_* call that fails with
+ * PC_ERR_COMPUTATION on a rank of a group does this itself, so an error one rank alone
+ * sees (HIP, HBM, a lost capability) ends every rank instead of leaving it waiting in a
+ * collective. A peer process that exits, or a collective that does not complete within
+ * PICARD_COMM_TIMEOUT_S seconds (default 600), aborts the group too. */
+void pc_ctx_abort(pc_ctx* ctx, const char* why);
+/* Free the context's HBM caches (the int8 digit image of X, the kept-Y buffer); later
+ * passes run without them (the fp64 Y stage, completion by recomputation). On a rank
+ * whose group agreed to use the digit image this makes its next screened try fail —
+ * and abort the group — rather than let the ranks diverge. */
+int pc_ctx_release_caches(pc_ctx* ctx, char* err, size_t errlen);
 /* copy a host shard (n_features × n_local, row-major) into HBM */
 int pc_ctx_load(pc_ctx* ctx, const double* x_shard, uint64_t n_features, uint64_t n_local,
                 uint64_t n_total, uint64_t t0, char* err, size_t errlen);

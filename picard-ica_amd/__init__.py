@@ -29,7 +29,7 @@ import numpy as np
 __all__ = [
     "Picard", "PicardConfig", "ConfigBuilder", "PicardResult", "DensityType", "PicardError",
     "InvalidDimensions", "SingularMatrix", "ComputationError", "InvalidConfig", "NotConverged",
-    "DeviceContext", "Solver", "utils", "lib", "LIB_PATH",
+    "DeviceContext", "LocalGroup", "Solver", "utils", "lib", "LIB_PATH",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -156,6 +156,13 @@ def _load():
         "pc_permute": (None, [d, u64, i32, d]),
         "pc_error_name": (C.c_char_p, [C.c_int]),
         "pc_version": (C.c_char_p, []),
+        "pc_abi_version": (C.c_int, []),
+        "pc_group_create_local": (C.c_int, [i32, P(vp), cp, sz]),
+        "pc_group_destroy": (None, [vp]),
+        "pc_ctx_create_in_group": (C.c_int, [i32, i32, vp, P(vp), cp, sz]),
+        "pc_ctx_comm_stats": (None, [vp, P(C.c_int64)]),
+        "pc_ctx_abort": (None, [vp, cp]),
+        "pc_ctx_release_caches": (C.c_int, [vp, cp, sz]),
         "pc_rccl_unique_id": (C.c_int, [cp]),
         "pc_ctx_create": (C.c_int, [i32, i32, i32, cp, P(vp), cp, sz]),
         "pc_ctx_destroy": (None, [vp]),
@@ -202,7 +209,9 @@ lib = _load()
 EXPORTED = [
     "pc_config_default", "pc_config_validate", "pc_fit", "pc_fit_default", "pc_transform",
     "pc_full_unmixing", "pc_mixing", "pc_result_free", "pc_amari_distance", "pc_permute",
-    "pc_error_name", "pc_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
+    "pc_error_name", "pc_version", "pc_abi_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
+    "pc_group_create_local", "pc_group_destroy", "pc_ctx_create_in_group", "pc_ctx_comm_stats", "pc_ctx_abort",
+    "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
     "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
@@ -482,15 +491,64 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
-class DeviceContext:
-    """pc_ctx: one GPU, one contiguous T shard of X resident in HBM."""
+class LocalGroup:
+    """pc_group: an in-process rank group — `world_size` DeviceContexts in this process,
+    one host thread per rank (they may share one GPU), that exchange every pass's
+    statistics through host memory (fixed rank-order sum) instead of RCCL. Runs the
+    communicator path of bench.py --gpus N (rank-replicated Solver, per-pass
+    all-reduce, capability agreements, group abort) on one device."""
 
-    def __init__(self, device: int = 0, rank: int = 0, world_size: int = 1, rccl_id: Optional[bytes] = None):
+    def __init__(self, world_size: int):
         h = C.c_void_p()
         err = _errbuf()
-        _raise(lib.pc_ctx_create(device, rank, world_size, rccl_id, C.byref(h), err, len(err)), err)
+        _raise(lib.pc_group_create_local(world_size, C.byref(h), err, len(err)), err)
+        self.h = h
+        self.world_size = world_size
+
+    def close(self):
+        if self.h:
+            lib.pc_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceContext:
+    """pc_ctx: one GPU, one contiguous T shard of X resident in HBM. With `group`
+    (a LocalGroup) the context is rank `rank` of that in-process group; with
+    world_size > 1 and an `rccl_id` it is one rank of an RCCL communicator; with
+    world_size > 1 and neither, a detached shard (partial sums)."""
+
+    def __init__(self, device: int = 0, rank: int = 0, world_size: int = 1, rccl_id: Optional[bytes] = None,
+                 group: Optional[LocalGroup] = None):
+        h = C.c_void_p()
+        err = _errbuf()
+        if group is not None:
+            _raise(lib.pc_ctx_create_in_group(device, rank, group.h, C.byref(h), err, len(err)), err)
+        else:
+            _raise(lib.pc_ctx_create(device, rank, world_size, rccl_id, C.byref(h), err, len(err)), err)
         self.h = h
         self.n_features = 0
+
+    def comm_stats(self) -> dict:
+        """pc_ctx_comm_stats: all-reduces issued, capability agreements asked and their outcome."""
+        o = (C.c_int64 * 7)()
+        lib.pc_ctx_comm_stats(self.h, o)
+        return {"allreduces": o[0], "agreements": o[1], "screen_agreed": o[2], "keep_y_agreed": o[3],
+                "aborted": bool(o[4]), "world_size": o[5], "kind": {0: None, 1: "rccl", 2: "local"}[o[6]]}
+
+    def abort(self, why: str = "aborted by the caller"):
+        """pc_ctx_abort: end every rank's pending and later collectives with an error."""
+        lib.pc_ctx_abort(self.h, why.encode())
+
+    def release_caches(self):
+        """pc_ctx_release_caches: free the int8 digit image and the kept-Y buffer."""
+        err = _errbuf()
+        _raise(lib.pc_ctx_release_caches(self.h, err, len(err)), err)
 
     def close(self):
         if self.h:

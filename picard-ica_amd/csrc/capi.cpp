@@ -6,6 +6,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <utility>
 
 #include "../../include/picard_mi355x.h"
 #include "evaluator.hpp"
@@ -13,7 +14,12 @@
 #include "host_solver.hpp"
 
 namespace pcamd {
-Evaluator* make_device_ctx(int device, int rank, int world, const char* uid);
+struct LocalGroup;
+std::shared_ptr<LocalGroup> make_local_group(int world);
+int local_group_world(const LocalGroup& g);
+Evaluator* make_device_ctx(int device, int rank, int world, const char* uid, std::shared_ptr<LocalGroup> grp);
+void device_ctx_comm_stats(const Evaluator* e, int64_t* out);
+void device_ctx_release_caches(Evaluator* e);
 void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0);
 void device_ctx_generate(Evaluator* e, uint64_t nf, uint64_t nt, uint64_t seed, double* a_out);
 void device_ctx_download(Evaluator* e, double* out);
@@ -39,6 +45,10 @@ struct pc_ctx {
 };
 struct pc_solver {
   std::unique_ptr<Solver> s;
+  Evaluator* ev = nullptr;  // the context it drives (group abort on failure)
+};
+struct pc_group {
+  std::shared_ptr<LocalGroup> g;
 };
 
 namespace {
@@ -61,6 +71,23 @@ int guarded(char* err, size_t errlen, F&& f) {
     set_err(err, errlen, std::string("Computation error: ") + e.what());
     return PC_ERR_COMPUTATION;
   }
+}
+
+// The same, for calls on a context of a rank group: an error this rank may be alone in
+// seeing (PC_ERR_COMPUTATION: HIP, HBM, a lost capability, a peer's abort) aborts the
+// group, so the other ranks' collectives end with an error instead of waiting for this
+// rank. Dimension / configuration errors are raised identically on every rank before
+// any collective and leave the group usable.
+template <class F>
+int guarded_on(Evaluator* ev, char* err, size_t errlen, F&& f) {
+  char local[512];
+  if (!err || !errlen) {
+    err = local;
+    errlen = sizeof local;
+  }
+  const int rc = guarded(err, errlen, std::forward<F>(f));
+  if (rc == PC_ERR_COMPUTATION && ev) ev->abort_group(err);
+  return rc;
 }
 
 // Evaluator over caller callbacks (pc_host_evaluator): host-logic tests only.
@@ -150,7 +177,7 @@ int pc_fit(const double* x, uint64_t nf, uint64_t ns, const pc_config* cfg, pc_r
     int rc = pc_config_validate(cfg, e2, sizeof e2);
     if (rc) throw PicardError(rc, e2);
     if (nf == 0 || ns == 0) throw invalid_dimensions("Input matrix cannot be empty");
-    std::unique_ptr<Evaluator> ev(make_device_ctx(cfg->device, 0, 1, nullptr));
+    std::unique_ptr<Evaluator> ev(make_device_ctx(cfg->device, 0, 1, nullptr, nullptr));
     device_ctx_load(ev.get(), x, nf, ns, ns, 0);
     Solver s(ev.get(), *cfg);
     while (!s.step()) {
@@ -182,7 +209,7 @@ int pc_transform(const double* x, uint64_t nf, uint64_t ns, const pc_result* res
   return guarded(err, errlen, [&] {
     Mat w = full_unmixing_of(res);
     if (w.cols != nf) throw invalid_dimensions("transform: n_features does not match the fitted model");
-    std::unique_ptr<Evaluator> ev(make_device_ctx(device, 0, 1, nullptr));
+    std::unique_ptr<Evaluator> ev(make_device_ctx(device, 0, 1, nullptr, nullptr));
     device_ctx_load(ev.get(), x, nf, ns, ns, 0);
     ev->sources(w.data(), w.rows, res->mean, out);
   });
@@ -279,7 +306,8 @@ const char* pc_error_name(int s) {
   }
 }
 
-const char* pc_version(void) { return "picard-mi355x 0.1.0 (reference picard-ica 0.1.6)"; }
+const char* pc_version(void) { return "picard-mi355x 0.3.0 (reference picard-ica 0.1.6)"; }
+int pc_abi_version(void) { return PC_ABI_VERSION; }
 
 int pc_rccl_unique_id(char id_out[128]) { return rccl_unique_id(id_out) ? PC_ERR_COMPUTATION : PC_OK; }
 
@@ -289,20 +317,61 @@ int pc_ctx_create(int32_t device, int32_t rank, int32_t world, const char* id, p
   return guarded(err, errlen, [&] {
     if (world < 1 || rank < 0 || rank >= world) throw invalid_dimensions("bad rank / world_size");
     auto* c = new pc_ctx;
-    c->ev.reset(make_device_ctx(device, rank, world, id));
+    try {
+      c->ev.reset(make_device_ctx(device, rank, world, id, nullptr));
+    } catch (...) {
+      delete c;
+      throw;
+    }
     *out = c;
   });
+}
+
+int pc_group_create_local(int32_t world, pc_group** out, char* err, size_t errlen) {
+  *out = nullptr;
+  return guarded(err, errlen, [&] {
+    auto* g = new pc_group;
+    g->g = make_local_group(world);
+    *out = g;
+  });
+}
+
+void pc_group_destroy(pc_group* g) { delete g; }
+
+int pc_ctx_create_in_group(int32_t device, int32_t rank, pc_group* g, pc_ctx** out, char* err, size_t errlen) {
+  *out = nullptr;
+  return guarded(err, errlen, [&] {
+    if (!g) throw invalid_dimensions("no rank group");
+    const int world = local_group_world(*g->g);
+    if (rank < 0 || rank >= world) throw invalid_dimensions("bad rank / world_size");
+    auto* c = new pc_ctx;
+    try {
+      c->ev.reset(make_device_ctx(device, rank, world, nullptr, g->g));
+    } catch (...) {
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+
+void pc_ctx_comm_stats(const pc_ctx* c, int64_t out[7]) { device_ctx_comm_stats(c->ev.get(), out); }
+
+void pc_ctx_abort(pc_ctx* c, const char* why) { c->ev->abort_group(why ? why : "aborted by the caller"); }
+
+int pc_ctx_release_caches(pc_ctx* c, char* err, size_t errlen) {
+  return guarded_on(c->ev.get(), err, errlen, [&] { device_ctx_release_caches(c->ev.get()); });
 }
 
 void pc_ctx_destroy(pc_ctx* c) { delete c; }
 
 int pc_ctx_load(pc_ctx* c, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0, char* err,
                 size_t errlen) {
-  return guarded(err, errlen, [&] { device_ctx_load(c->ev.get(), x, nf, nl, nt, t0); });
+  return guarded_on(c->ev.get(), err, errlen, [&] { device_ctx_load(c->ev.get(), x, nf, nl, nt, t0); });
 }
 
 int pc_ctx_generate(pc_ctx* c, uint64_t nf, uint64_t nt, uint64_t seed, double* a_out, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] { device_ctx_generate(c->ev.get(), nf, nt, seed, a_out); });
+  return guarded_on(c->ev.get(), err, errlen, [&] { device_ctx_generate(c->ev.get(), nf, nt, seed, a_out); });
 }
 
 int pc_ctx_download(pc_ctx* c, double* out) {
@@ -319,7 +388,7 @@ uint64_t pc_ctx_t0(const pc_ctx* c) { return device_ctx_t0(c->ev.get()); }
 
 int pc_ctx_eval(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density d, uint32_t flags,
                 double* stats, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
     c->ev->want_y2 = (flags & PC_EVAL_SKIP_Y2) == 0;
@@ -329,7 +398,7 @@ int pc_ctx_eval(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_de
 
 int pc_ctx_eval_loss(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density d, uint32_t flags,
                      double* stats, int32_t* kept, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
     const bool h = (flags & PC_EVAL_NEED_H) != 0;
@@ -344,7 +413,7 @@ int pc_ctx_eval_loss(pc_ctx* c, const double* w, uint64_t nc, const double* mu, 
 int pc_ctx_eval_loss_multi(pc_ctx* c, const double* w, const double* z, uint64_t nc, const double* mu,
                            pc_density d, const double* alphas, uint64_t n_alpha, double* ll_out, double* y2_out,
                            char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
     if (n_alpha == 0) return;
@@ -354,28 +423,28 @@ int pc_ctx_eval_loss_multi(pc_ctx* c, const double* w, const double* z, uint64_t
 }
 
 int pc_ctx_eval_complete(pc_ctx* c, pc_density d, uint32_t flags, double* stats, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     // only the entries [G | H | Σψ′] are written; Σℓ, Σy² of `stats` are left as they are
     c->ev->eval_complete_into(d, (flags & PC_EVAL_NEED_H) != 0, stats);
   });
 }
 
 int pc_ctx_rowsum(pc_ctx* c, double* out, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] { c->ev->rowsum(out); });
+  return guarded_on(c->ev.get(), err, errlen, [&] { c->ev->rowsum(out); });
 }
 
 int pc_ctx_gram(pc_ctx* c, const double* mu, double* out, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] { c->ev->gram(mu, out); });
+  return guarded_on(c->ev.get(), err, errlen, [&] { c->ev->gram(mu, out); });
 }
 
 int pc_ctx_sources(pc_ctx* c, const double* w, uint64_t nc, const double* mu, double* out, char* err,
                    size_t errlen) {
-  return guarded(err, errlen, [&] { c->ev->sources(w, nc, mu, out); });
+  return guarded_on(c->ev.get(), err, errlen, [&] { c->ev->sources(w, nc, mu, out); });
 }
 
 int pc_ctx_sources_device(pc_ctx* c, const double* w, uint64_t nc, const double* mu, const double** dev_out,
                           uint64_t* ld_out, double* kernel_ms, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     uint64_t ld = 0;
     double ms = 0.0;
     const double* p = device_ctx_sources_resident(c->ev.get(), w, nc, mu, &ms, &ld);
@@ -387,7 +456,7 @@ int pc_ctx_sources_device(pc_ctx* c, const double* w, uint64_t nc, const double*
 
 int pc_ctx_moments4(pc_ctx* c, const double* w, uint64_t nc, const double* mu, double* out, char* err,
                     size_t errlen) {
-  return guarded(err, errlen, [&] { c->ev->moments4(w, nc, mu, out); });
+  return guarded_on(c->ev.get(), err, errlen, [&] { c->ev->moments4(w, nc, mu, out); });
 }
 
 void pc_ctx_last_timing(const pc_ctx* c, double* k, double* call) { device_ctx_timing(c->ev.get(), k, call); }
@@ -410,7 +479,7 @@ uint64_t pc_ctx_int8_passes(const pc_ctx* c) { return device_ctx_int8_passes(c->
 
 int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density density,
                             double* ll_out, double* bound_out, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     if (!c->ev->eval_loss_screen(w, nc, mu, density, ll_out, bound_out))
       throw computation_error("no line-search screen for this shape / density");
   });
@@ -431,9 +500,13 @@ int pc_device_synchronize(int32_t device) {
 
 int pc_ctx_jade(pc_ctx* c, const double* w, uint64_t nc, const double* mu, uint64_t max_iter, double tol,
                 int32_t where, double* w_out, uint64_t sweeps_out[3], char* err, size_t errlen) {
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     const uint64_t nf = c->ev->n_features();
     if (nc == 0 || nc > nf) throw invalid_dimensions("n_components must be in 1..=n_features");
+    // the cumulants need the fourth moments of ALL samples: a detached shard only has its own
+    if (c->ev->partial_sums())
+      throw invalid_config("ctx", "a detached shard context returns partial moments; sum pc_ctx_moments4 over the "
+                                  "shards and run the sweeps on the host");
     if (where < PC_JADE_AUTO || where > PC_JADE_HOST) throw invalid_config("where", "unknown sweep placement");
     Mat base(nc, nf);
     std::memcpy(base.data(), w, nc * nf * sizeof(double));
@@ -451,7 +524,7 @@ int pc_ctx_jade(pc_ctx* c, const double* w, uint64_t nc, const double* mu, uint6
 
 int pc_solver_create(pc_ctx* c, const pc_config* cfg, pc_solver** out, char* err, size_t errlen) {
   *out = nullptr;
-  return guarded(err, errlen, [&] {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
     char e2[512];
     int rc = pc_config_validate(cfg, e2, sizeof e2);
     if (rc) throw PicardError(rc, e2);
@@ -459,6 +532,7 @@ int pc_solver_create(pc_ctx* c, const pc_config* cfg, pc_solver** out, char* err
       throw invalid_config("ctx", "a detached shard context (world_size > 1 without an RCCL id) returns partial "
                                   "sums; drive the shards with pc_fit_with_evaluator");
     auto* s = new pc_solver;
+    s->ev = c->ev.get();
     try {
       s->s.reset(new Solver(c->ev.get(), *cfg));
     } catch (...) {
@@ -470,12 +544,12 @@ int pc_solver_create(pc_ctx* c, const pc_config* cfg, pc_solver** out, char* err
 }
 
 int pc_solver_step(pc_solver* s, int32_t* done, char* err, size_t errlen) {
-  return guarded(err, errlen, [&] { *done = s->s->step() ? 1 : 0; });
+  return guarded_on(s->ev, err, errlen, [&] { *done = s->s->step() ? 1 : 0; });
 }
 
 int pc_solver_finish(pc_solver* s, pc_result* out, char* err, size_t errlen) {
   std::memset(out, 0, sizeof *out);
-  return guarded(err, errlen, [&] { s->s->finish(out); });
+  return guarded_on(s->ev, err, errlen, [&] { s->s->finish(out); });
 }
 
 void pc_solver_destroy(pc_solver* s) { delete s; }

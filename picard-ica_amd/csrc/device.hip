@@ -14,17 +14,19 @@
 // sums are reduced by k_reduce in a fixed order (bit-reproducible; no atomics).
 #include <hip/hip_runtime.h>
 #include <hip/hip_cooperative_groups.h>
-#include <rccl/rccl.h>
-
 #include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
+#include "collective.hpp"
 #include "evaluator.hpp"
 #include "host_linalg.hpp"
 
@@ -46,13 +48,6 @@ enum { DENS_TANH = 0, DENS_EXP = 1, DENS_CUBE = 2, DENS_LINEAR = 3, DENS_NONE = 
     hipError_t e_ = (expr);                                                                \
     if (e_ != hipSuccess)                                                                  \
       throw computation_error(std::string("HIP: ") + hipGetErrorString(e_) + " at " #expr); \
-  } while (0)
-
-#define RCCL_OK(expr)                                                                        \
-  do {                                                                                       \
-    ncclResult_t r_ = (expr);                                                                \
-    if (r_ != ncclSuccess)                                                                   \
-      throw computation_error(std::string("RCCL: ") + ncclGetErrorString(r_) + " at " #expr); \
   } while (0)
 
 // ---------------------------------------------------------------------------
@@ -1996,13 +1991,30 @@ __global__ void k_gen_sources(double* __restrict__ S, uint64_t lds, int nf, uint
   }
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), raised when a
+// larger size is asked for; thread-safe (the rank contexts of an in-process group launch
+// from their own host threads)
+static void lds_attr(const void* f, int bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> set;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  int& have = set[{f, dev}];
+  if (bytes > have) {
+    HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    have = bytes;
+  }
+}
+
 // ---------------------------------------------------------------------------
-// Device context: one GPU, one X shard, optional RCCL communicator.
+// Device context: one GPU, one X shard, optional collective (RCCL, or an
+// in-process rank group; collective.hpp).
 // ---------------------------------------------------------------------------
 struct DeviceCtx : Evaluator {
   int device = 0, rank = 0, world = 1;
   hipStream_t stream = nullptr;
-  ncclComm_t comm = nullptr;
+  std::unique_ptr<Collective> coll_;
   double* X = nullptr;
   uint64_t nf = 0, n_local_ = 0, ldx = 0, n_total = 0, t0 = 0;
   int n_cu = 256;
@@ -2045,24 +2057,23 @@ struct DeviceCtx : Evaluator {
     sl.pending = true;
   }
 
-  DeviceCtx(int dev, int rk, int ws, const char* uid) : device(dev), rank(rk), world(ws) {
+  DeviceCtx(int dev, int rk, int ws, const char* uid, std::shared_ptr<LocalGroup> grp)
+      : device(dev), rank(rk), world(ws) {
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
     n_cu = prop.multiProcessorCount;
-    // world > 1 without an RCCL id: a detached shard (no communicator; every
+    // world > 1 without an RCCL id or a group: a detached shard (no communicator; every
     // statistic is this shard's partial sum and the caller adds them up)
-    if (world > 1 && uid) {
-      ncclUniqueId id;
-      std::memcpy(&id, uid, sizeof id);
-      RCCL_OK(ncclCommInitRank(&comm, world, id, rank));
-    }
+    if (grp) coll_ = make_local_collective(std::move(grp), rank);
+    else if (world > 1 && uid) coll_ = make_rccl_collective(rank, world, uid);
+    if (const char* e = std::getenv("PICARD_TEST_PIN_DIGITS")) pin_test_ = std::atoi(e) != 0;
   }
   ~DeviceCtx() override {
     (void)hipSetDevice(device);
-    if (comm) ncclCommDestroy(comm);
+    coll_.reset();
     for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src})
       if (p) (void)hipFree(p);
     for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsl, (void*)d_wsc})
@@ -2079,7 +2090,15 @@ struct DeviceCtx : Evaluator {
   uint64_t n_features() const override { return nf; }
   uint64_t n_samples() const override { return n_total; }
   uint64_t n_local() const override { return n_local_; }
-  bool partial_sums() const override { return world > 1 && !comm; }
+  bool partial_sums() const override { return world > 1 && !coll_; }
+  void abort_group(const std::string& why) noexcept override {
+    if (coll_) coll_->abort(why);
+  }
+  // wait for this context's stream; with a collective, a failing peer ends the wait
+  void sync() {
+    if (coll_) coll_->wait(stream);
+    else HIP_OK(hipStreamSynchronize(stream));
+  }
 
   double* ensure(double*& p, size_t& cap, size_t n) {
     if (n > cap) {
@@ -2088,7 +2107,10 @@ struct DeviceCtx : Evaluator {
       cap = 0;
       if (hipMalloc(&p, n * sizeof(double)) != hipSuccess) {
         (void)hipGetLastError();
-        release_xsl();  // the int8 slice image is a cache: its HBM goes to the pass buffers
+        // the int8 slice image is a cache: its HBM goes to the pass buffers — unless the
+        // ranks agreed on it (the screen branch issues its own collectives): then the
+        // allocation fails instead and the group aborts rather than diverging
+        if (!xsl_pinned()) release_xsl();
         HIP_OK(hipMalloc(&p, n * sizeof(double)));
       }
       cap = n;
@@ -2116,7 +2138,7 @@ struct DeviceCtx : Evaluator {
     if (n_local)
       HIP_OK(hipMemcpy2DAsync(X, ldx * sizeof(double), xh, n_local * sizeof(double), n_local * sizeof(double),
                               nf, hipMemcpyHostToDevice, stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
   }
 
   void download(double* out) {
@@ -2125,7 +2147,7 @@ struct DeviceCtx : Evaluator {
     if (n_local_)
       HIP_OK(hipMemcpy2DAsync(out, n_local_ * sizeof(double), X, ldx * sizeof(double), n_local_ * sizeof(double),
                               nf, hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
   }
 
   static uint64_t shard_t0(uint64_t n_tot, int world, int rank) {
@@ -2160,11 +2182,11 @@ struct DeviceCtx : Evaluator {
       // X[:, c0:c0+cn] = A·S (benchmarks.rs:34) on MFMA; the padding past n_local stays zero
       ystore_run(S, CH, nf, nf, cn, X + c0, ldx);
     }
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
   }
 
-  void allreduce(double* d, size_t n) {
-    if (comm) RCCL_OK(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm, stream));
+  void allreduce(double* d, size_t n, const char* tag) {
+    if (coll_) coll_->allreduce(d, n, stream, tag);
   }
 
   // ---- Y = W·Xs stored row-major on MFMA (k_ystore) ------------------------
@@ -2175,12 +2197,7 @@ struct DeviceCtx : Evaluator {
   template <int KS>
   void ystore_ks_launch(const double* Xs, uint64_t lds, uint64_t nrows, const double* dwt, int ncp, size_t nc,
                         uint64_t n_out, double* Y, uint64_t ldy) {
-    static bool attr = false;
-    if (!attr) {
-      HIP_OK(hipFuncSetAttribute((const void*)k_ystore<KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 4 * 16 * 4 * KS * (int)sizeof(double)));
-      attr = true;
-    }
+    lds_attr((const void*)k_ystore<KS>, 4 * 16 * 4 * KS * (int)sizeof(double));
     const uint64_t n_blocks = (n_out + 15) / 16;
     const int nroles = (ncp / 16 + 7) / 8;
     // two workgroups per CU in ONE round (a 2·n_cu + 1-th would run alone afterwards)
@@ -2203,7 +2220,7 @@ struct DeviceCtx : Evaluator {
       for (size_t k = 0; k < nrows; ++k) wt[k * ncp + i] = w[i * nrows + k];
     ensure(d_wys, cap_wys, wt.size());
     HIP_OK(hipMemcpyAsync(d_wys, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipStreamSynchronize(stream));  // the host image must outlive the copy; the kernels stay async
+    sync();  // the host image must outlive the copy; the kernels stay async
   }
   // Y[:, :n_out] = W·Xs with the map of the last ystore_upload (same nc, nrows)
   void ystore_run(const double* Xs, uint64_t lds, uint64_t nrows, size_t nc, uint64_t n_out, double* Y, uint64_t ldy) {
@@ -2237,9 +2254,9 @@ struct DeviceCtx : Evaluator {
     if (xshift_.empty()) local_rowsum(st, d_part, cap_part);
     else  // centred in place: the sums of the caller's data, kept from before the shift
       HIP_OK(hipMemcpyAsync(st, raw_sums_.data(), nf * sizeof(double), hipMemcpyHostToDevice, stream));
-    allreduce(st, nf);
+    allreduce(st, nf, "rowsum");
     HIP_OK(hipMemcpyAsync(out, st, nf * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
   }
 
   // Resident-X centring. Every pass computes Y = W·(X − μ); instead of
@@ -2262,7 +2279,7 @@ struct DeviceCtx : Evaluator {
     if (undo) k_shift_rows<true><<<dim3(gx, (unsigned)nf), 256, 0, stream>>>(X, ldx, n_local_, dmu);
     else k_shift_rows<false><<<dim3(gx, (unsigned)nf), 256, 0, stream>>>(X, ldx, n_local_, dmu);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(stream));  // the host μ buffer may go away after return
+    sync();  // the host μ buffer may go away after return
   }
   void unshift_x() {
     if (xshift_.empty()) return;
@@ -2327,16 +2344,12 @@ struct DeviceCtx : Evaluator {
     // NB = 8 without H: the warp-specialised 16-wave kernel (same sums as k_eval_fused<8>),
     // on the int8-digit Y stage when the digit image is there (not for the Gram)
     const bool ws = NB == 8 && !H;
-    const bool oz = ws && D != DENS_LINEAR && dmu == nullptr && oz_fused_ready_;
+    // (after the partial buffer: an allocation that released the digit image falls back to
+    // the fp64 Y stage, which issues the same collectives)
+    const bool oz = ws && D != DENS_LINEAR && dmu == nullptr && oz_fused_ready_ && xsl_valid_;
     auto kws = oz ? k_eval_fused_ws<D, Q, true> : k_eval_fused_ws<D, Q, false>;
     auto kfu = k_eval_fused<NB, H, D, Q>;
-    static bool attr_set[3] = {false, false, false};
-    const int ak = ws ? (oz ? 2 : 1) : 0;
-    if (!attr_set[ak]) {
-      HIP_OK(hipFuncSetAttribute(ws ? (const void*)kws : (const void*)kfu, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 160 * 1024 - EXP_TAB_BYTES));
-      attr_set[ak] = true;
-    }
+    lds_attr(ws ? (const void*)kws : (const void*)kfu, 160 * 1024 - EXP_TAB_BYTES);
     HIP_OK(hipEventRecord(ev[1], stream));
     if (ws)
       kws<<<nwg, WS_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part, d_xsl, d_xsc,
@@ -2413,10 +2426,10 @@ struct DeviceCtx : Evaluator {
     } else {
       throw computation_error("no evaluation path for density id " + std::to_string(dens));
     }
-    allreduce(st, total);
+    allreduce(st, total, need_h ? "eval+H" : "eval");
     HIP_OK(hipMemcpyAsync(stats_host, st, total * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipEventRecord(ev[3], stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
     float a = 0, b = 0;
     const bool timed = fused || tiled;  // "fused" kind = every full pass (fused or tiled)
     if (timed) { HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2])); }
@@ -2435,11 +2448,7 @@ struct DeviceCtx : Evaluator {
     const int nroles = (ncp / 16 + 3) / 4;
     const size_t lds = (size_t)(2 * 16 * 4 * KS + 2 * 2 * 4 * 2 * 4 * 64) * sizeof(double);
     auto k = want_y2 ? k_multi_loss2<KS, D, true> : k_multi_loss2<KS, D, false>;
-    static bool attr[2] = {false, false};
-    if (!attr[want_y2]) {
-      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
-      attr[want_y2] = true;
-    }
+    lds_attr((const void*)k, 160 * 1024 - EXP_TAB_BYTES);
     k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, ncp, dw, dz, dmu, alpha, dal, na,
                                                              bpw, n_blocks, part, (uint64_t)nwg);
   }
@@ -2515,7 +2524,7 @@ struct DeviceCtx : Evaluator {
     multi_finish(st, nc, na, ll_out, y2_out);
   }
   void multi_finish(double* st, size_t nc, int na, double* ll_out, double* y2_out) {
-    allreduce(st, (size_t)2 * na * nc);
+    allreduce(st, (size_t)2 * na * nc, "loss_multi");
     std::vector<double> h((size_t)2 * na * nc);
     HIP_OK(hipMemcpyAsync(h.data(), st, h.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
     finish_timing(true, 3);
@@ -2569,11 +2578,7 @@ struct DeviceCtx : Evaluator {
                        : (mode == 0 ? k_tiled_yw<KS, D, 0, false> : mode == 1 ? k_tiled_yw<KS, D, 1, false>
                                                                              : k_tiled_yw<KS, D, 2, false>);
     if (yin && !YC) throw computation_error("tiled pass: feature chunks need KS = 64");
-    static bool attr[2][3] = {{false, false, false}, {false, false, false}};
-    if (!attr[yin != nullptr][mode]) {
-      HIP_OK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - EXP_TAB_BYTES));
-      attr[yin != nullptr][mode] = true;
-    }
+    lds_attr((const void*)k, 160 * 1024 - EXP_TAB_BYTES);
     k<<<xcd_grid(nwg1, nroles), FUSED_THREADS, lds, stream>>>(X0, ldx, 0, (int)nrows, ncp, wpt, nullptr, alpha, bpw,
                                                               n_blocks, d_trow, acc ? 1 : 0, yb, pb, db, yin,
                                                               (uint64_t)nwg1);
@@ -2608,12 +2613,8 @@ struct DeviceCtx : Evaluator {
       const int nto = (ncp / 16 + 7) / 8;
       const uint64_t tps = (ntl + nsplit - 1) / nsplit;
       const size_t lds2 = (size_t)2 * (db ? 3 : 2) * 8 * 256 * sizeof(double);
-      static bool attr2[2] = {false, false};
       auto k2 = !need_h ? k_tiled_gram2<false, false> : dfromp ? k_tiled_gram2<true, true> : k_tiled_gram2<true, false>;
-      if (!attr2[need_h]) {
-        HIP_OK(hipFuncSetAttribute((const void*)k2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr2[need_h] = true;
-      }
+      lds_attr((const void*)k2, 160 * 1024);
       k2<<<xcd_grid(nsplit, nto * nto), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0,
                                                                        alpha, (uint64_t)nsplit);
       HIP_OK(hipGetLastError());
@@ -2726,6 +2727,10 @@ struct DeviceCtx : Evaluator {
   bool ensure_xsl() {
     if (xsl_valid_) return true;
     if (xsl_failed_) return false;
+    // the scratch of the Σ 2^e_t sum first: an allocation here may release the image
+    const int nwg_e = (int)std::max<uint64_t>(1, std::min<uint64_t>((ldx + 4095) / 4096, 1024));
+    ensure(d_shift_part, cap_shift_part, (size_t)nwg_e + 1);
+    if (xsl_failed_) return false;
     const uint64_t n_blocks = ldx / 16;
     const size_t need = (size_t)n_blocks * OZ_BLOCK_BYTES;
     if (need > cap_xsl) {
@@ -2748,15 +2753,15 @@ struct DeviceCtx : Evaluator {
     k_slice_x<<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     HIP_OK(hipGetLastError());
     {  // Σ_t 2^e_t of this shard (padding included: it only loosens the screen's bound)
-      const int nwg = (int)std::max<uint64_t>(1, std::min<uint64_t>((ldx + 4095) / 4096, 1024));
+      const int nwg = nwg_e;
       const uint64_t per = ((ldx + nwg - 1) / nwg + 511) / 512 * 512;
-      double* part = ensure(d_shift_part, cap_shift_part, (size_t)nwg + 1);
+      double* part = d_shift_part;
       k_rowsum<<<dim3((unsigned)((ldx + per - 1) / per), 1), 256, 0, stream>>>(d_xsc, ldx, ldx, 1, per, part);
       HIP_OK(hipGetLastError());
       k_sum_slabs<<<1, 256, 0, stream>>>(part, (int)((ldx + per - 1) / per), 1, part + nwg);
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(&xsc_sum_, part + nwg, sizeof(double), hipMemcpyDeviceToHost, stream));
-      HIP_OK(hipStreamSynchronize(stream));
+      sync();
     }
     xsl_valid_ = true;
     return true;
@@ -2793,13 +2798,11 @@ struct DeviceCtx : Evaluator {
     uint64_t bpw;
     const int nwg = partition(n_blocks, &bpw);
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * 128);
+    // never launch on a released image (callers allocate their buffers before relying on it)
+    if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
     const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
     auto kern = store ? k_eval_loss_oz<D, true, Q, DMAX> : k_eval_loss_oz<D, false, Q, DMAX>;
-    static bool attr[2] = {false, false};
-    if (!attr[store]) {
-      HIP_OK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr[store] = true;
-    }
+    lds_attr((const void*)kern, (int)lds);
     HIP_OK(hipEventRecord(ev[1], stream));
     kern<<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, alpha, bpw, n_blocks, part,
                                               store ? d_ybuf : nullptr);
@@ -2822,11 +2825,7 @@ struct DeviceCtx : Evaluator {
     uint64_t bpw;
     const int nwg = partition(n_blocks, &bpw);
     const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
-    static bool attr = false;
-    if (!attr) {
-      HIP_OK(hipFuncSetAttribute((const void*)k_ystore_oz, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr = true;
-    }
+    lds_attr((const void*)k_ystore_oz, (int)lds);
     k_ystore_oz<<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, b_first, bpw, n_blocks, n_out, (int)nc,
                                                    Y, ldy);
     HIP_OK(hipGetLastError());
@@ -2837,19 +2836,28 @@ struct DeviceCtx : Evaluator {
   // later calls reuse the answer, and a rank that loses the capability afterwards
   // raises instead of diverging. state: 0 not asked, 1 all have it, -1 some do not.
   int screen_agreed_ = 0, ybuf_agreed_ = 0;
-  bool agree_once(int& state, bool local) {
+  uint64_t n_agree_ = 0;
+  bool pin_test_ = false;  // PICARD_TEST_PIN_DIGITS=1: pin the image without a group (tests)
+  bool xsl_pinned() const { return (coll_ && screen_agreed_ == 1) || pin_test_; }
+  bool agree_once(int& state, bool local, const char* what) {
     if (state == 0) {
+      ++n_agree_;
       double* f = ensure(d_shift_sum, cap_shift_sum, std::max<size_t>(nf, 1));  // scratch (not d_stats)
       const double one = local ? 1.0 : 0.0;
       HIP_OK(hipMemcpyAsync(f, &one, sizeof(double), hipMemcpyHostToDevice, stream));
-      allreduce(f, 1);
+      allreduce(f, 1, "agree");
       double all = 0.0;
       HIP_OK(hipMemcpyAsync(&all, f, sizeof(double), hipMemcpyDeviceToHost, stream));
-      HIP_OK(hipStreamSynchronize(stream));
+      sync();
       state = all == (double)world ? 1 : -1;
     }
     if (state < 0) return false;
-    if (!local) throw computation_error("a capability the ranks agreed on (int8 digit image / kept Y) was lost on this rank");
+    if (!local) {
+      // the other ranks take the agreed branch: end the group instead of diverging
+      const std::string m = std::string("the ranks agreed on ") + what + " but rank " + std::to_string(rank) + " lost it";
+      abort_group(m);
+      throw computation_error(m);
+    }
     return true;
   }
 
@@ -2867,15 +2875,20 @@ struct DeviceCtx : Evaluator {
       return false;
     HIP_OK(hipSetDevice(device));
     const double* dmu = resident_mu(mu);
+    double* st_rows = ensure(d_stats, cap_stats, 2 * nc);
+    {  // the pass buffers before the image is relied on (an allocation may release it)
+      uint64_t bpw0;
+      const int nwg0 = partition((n_local_ + 15) / 16, &bpw0);
+      ensure(d_part, cap_part, (size_t)nwg0 * 2 * 128);
+    }
     bool ok = dmu == nullptr && ensure_xsl();
     // With a communicator every rank must take the same branch (a screen and a full pass
     // issue different all-reduces): the ranks agree once on availability (the digit image
     // is a per-rank allocation).
-    if (comm) ok = agree_once(screen_agreed_, ok);
+    if (coll_) ok = agree_once(screen_agreed_, ok, "the int8 digit image (line-search screen)");
     if (!ok) return false;
     upload_wsl(w, nc);
     d_wsl_ready_ = true;
-    double* st_rows = ensure(d_stats, cap_stats, 2 * nc);
     kept_nc_pending = nc;
     HIP_OK(hipEventRecord(ev[0], stream));
     if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
@@ -2905,7 +2918,7 @@ struct DeviceCtx : Evaluator {
       bnd[i] = std::ldexp(tail, e - 12) * (1.0 + 1e-12);
     }
     HIP_OK(hipMemcpyAsync(st_rows + nc, bnd.data(), nc * sizeof(double), hipMemcpyHostToDevice, stream));
-    allreduce(st_rows, 2 * nc);
+    allreduce(st_rows, 2 * nc, "screen");
     std::vector<double> tmp(2 * nc);
     HIP_OK(hipMemcpyAsync(tmp.data(), st_rows, 2 * nc * sizeof(double), hipMemcpyDeviceToHost, stream));
     finish_timing(true, 4);
@@ -2925,8 +2938,13 @@ struct DeviceCtx : Evaluator {
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
     if constexpr (NB == 8) {
       if (dmu == nullptr && oz_shape(kept_nc_pending) && d_wsl_ready_) {
-        launch_loss_oz<D, Q>(alpha, store, st_rows);
-        return;
+        uint64_t bpw0;
+        const int nwg0 = partition(n_blocks, &bpw0);
+        ensure(d_part, cap_part, (size_t)nwg0 * 2 * 128);  // may release an unpinned image …
+        if (xsl_valid_) {  // … then the fp64 stage below runs (same collectives)
+          launch_loss_oz<D, Q>(alpha, store, st_rows);
+          return;
+        }
       }
     }
     uint64_t bpw;
@@ -2987,7 +3005,7 @@ struct DeviceCtx : Evaluator {
   uint64_t n_loss = 0, n_fromy = 0;
   void finish_timing(bool kernel_timed, int kind = 0) {
     HIP_OK(hipEventRecord(ev[3], stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
     float a = 0, b = 0;
     if (kernel_timed) HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2]));
     HIP_OK(hipEventElapsedTime(&b, ev[0], ev[3]));
@@ -3022,7 +3040,7 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipEventRecord(ev[1], stream));
       tiled_eval(w, nc, dmu, d.kind, d.alpha, need_h, st, 1);
       HIP_OK(hipEventRecord(ev[2], stream));
-      allreduce(st + total - 2 * nc, 2 * nc);
+      allreduce(st + total - 2 * nc, 2 * nc, "loss");
       HIP_OK(hipMemcpyAsync(out->buf.data() + total - 2 * nc, st + total - 2 * nc, 2 * nc * sizeof(double),
                             hipMemcpyDeviceToHost, stream));
       finish_timing(true, 1);
@@ -3041,7 +3059,7 @@ struct DeviceCtx : Evaluator {
     // With a communicator the ranks agree (once) on keeping Y: the two completions issue
     // different all-reduces.
     bool store = keep && ensure_ybuf(nb);
-    if (comm && keep) store = agree_once(ybuf_agreed_, store);
+    if (coll_ && keep) store = agree_once(ybuf_agreed_, store, "a kept Y buffer (completion from Y)");
     out->nc = nc;
     out->has_h = need_h;
     out->buf.assign(EvalStats::size(nc, need_h), 0.0);
@@ -3076,7 +3094,7 @@ struct DeviceCtx : Evaluator {
       default: if (q) { PC_LOSS(8, true); } else { PC_LOSS(8, false); } break;
     }
 #undef PC_LOSS
-    allreduce(st_rows, 2 * nc);
+    allreduce(st_rows, 2 * nc, "loss");
     HIP_OK(hipMemcpyAsync(out->buf.data() + total - 2 * nc, st_rows, 2 * nc * sizeof(double),
                           hipMemcpyDeviceToHost, stream));
     finish_timing(true, 1);
@@ -3145,7 +3163,7 @@ struct DeviceCtx : Evaluator {
       case 4: dispatch_fromy<4>(d, need_h, st); break;
       default: dispatch_fromy<8>(d, need_h, st); break;
     }
-    allreduce(st, e1);
+    allreduce(st, e1, need_h ? "complete+H" : "complete");
     HIP_OK(hipMemcpyAsync(out->buf.data(), st, e1 * sizeof(double), hipMemcpyDeviceToHost, stream));
     finish_timing(true, 2);
   }
@@ -3165,7 +3183,7 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipMemcpy2DAsync(out + c0, n_local_ * sizeof(double), Y, CH * sizeof(double), cn * sizeof(double), nc,
                               hipMemcpyDeviceToHost, stream));
     }
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
   }
 
   // Sources kept in HBM (S = W·(X − μ), nc × ldx, row-major, zero padding past
@@ -3185,7 +3203,7 @@ struct DeviceCtx : Evaluator {
     if (oz) ystore_oz_run(0, n_local_, nc, S, ldx);
     else ystore_run(X, ldx, nf, nc, n_local_, S, ldx);
     HIP_OK(hipEventRecord(ev[2], stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
     float a = 0;
     HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2]));
     if (kernel_ms) *kernel_ms = a;
@@ -3208,7 +3226,7 @@ struct DeviceCtx : Evaluator {
     int coop = 0;
     HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
     if (!coop) return false;
-    HIP_OK(hipFuncSetAttribute((const void*)k_jade_sweeps, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    lds_attr((const void*)k_jade_sweeps, (int)lds);
     int per_cu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_jade_sweeps, JS_THREADS, lds));
     if ((size_t)per_cu * n_cu < G) return false;
@@ -3240,7 +3258,7 @@ struct DeviceCtx : Evaluator {
     int sw[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(v_out, d_v, n * n * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipMemcpyAsync(sw, d_sw, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
     log->sweeps = (size_t)sw[0];
     log->converged = sw[1] != 0;
     log->theta10.assign(std::min<size_t>(log->sweeps / 10, (size_t)theta_cap), 0.0);
@@ -3316,7 +3334,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(dtm, tmask.data(), tmask.size(), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemsetAsync(acc, 0, (size_t)np * np * sizeof(double), stream));
     // the host image vectors must outlive the async copies
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
     const int tiles = (np + 31) / 32;
     bool first = true;
     for (uint64_t c0 = 0; c0 < n_local_; c0 += CH) {
@@ -3326,11 +3344,7 @@ struct DeviceCtx : Evaluator {
         const uint64_t nsb = (cn + 15) / 16;
         const uint64_t spb = (nsb + nsplit - 1) / nsplit;
         const size_t lds = (size_t)(2 * 64 * 16 + 2 * 2 * 8 * 4 * 64) * sizeof(double);
-        static bool attr = false;
-        if (!attr) {
-          HIP_OK(hipFuncSetAttribute((const void*)k_moments4_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-          attr = true;
-        }
+        lds_attr((const void*)k_moments4_mfma, (int)lds);
         k_moments4_mfma<<<(unsigned)(ntile * nsplit), FUSED_THREADS, lds, stream>>>(
             Y, CH, cn, (int)nc, dri, drj, dci, dcj, np, dtp, dtq, nsplit, spb, slabs, slab_stride);
         HIP_OK(hipGetLastError());
@@ -3342,13 +3356,13 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipGetLastError());
       first = false;
     }
-    allreduce(acc, (size_t)np * np);
+    allreduce(acc, (size_t)np * np, "moments4");
     if (mfma_path) {
       k_moments4_fill<<<(unsigned)(((size_t)np * np + 255) / 256), 256, 0, stream>>>(acc, dpi, dpj, (int)nc, np, full);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipMemcpyAsync(out, full, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    sync();
     if (!mfma_path)
       for (int p = 0; p < np; ++p)  // mirror the upper tiles
         for (int q = 0; q < p; ++q) out[(size_t)p * np + q] = out[(size_t)q * np + p];
@@ -3357,8 +3371,34 @@ struct DeviceCtx : Evaluator {
 };
 
 // factory + thin accessors used by capi.cpp
-Evaluator* make_device_ctx(int device, int rank, int world, const char* uid) {
-  return new DeviceCtx(device, rank, world, uid);
+Evaluator* make_device_ctx(int device, int rank, int world, const char* uid, std::shared_ptr<LocalGroup> grp) {
+  return new DeviceCtx(device, rank, world, uid, std::move(grp));
+}
+// [0] all-reduces issued, [1] capability agreements asked, [2] screen agreement, [3] kept-Y
+// agreement (0 not asked, 1 every rank, -1 not every rank), [4] 1 if the group was aborted,
+// [5] world size, [6] 1 RCCL / 2 in-process group / 0 none
+void device_ctx_comm_stats(const Evaluator* e, int64_t* out) {
+  auto* d = static_cast<const DeviceCtx*>(e);
+  out[0] = d->coll_ ? (int64_t)d->coll_->n_allreduce : 0;
+  out[1] = (int64_t)d->n_agree_;
+  out[2] = d->screen_agreed_;
+  out[3] = d->ybuf_agreed_;
+  out[4] = d->coll_ && d->coll_->aborted() ? 1 : 0;
+  out[5] = d->world;
+  out[6] = !d->coll_ ? 0 : std::strcmp(d->coll_->kind(), "rccl") == 0 ? 1 : 2;
+}
+// drop the HBM caches (int8 digit image, kept-Y buffer): later passes run without them
+void device_ctx_release_caches(Evaluator* e) {
+  auto* d = static_cast<DeviceCtx*>(e);
+  HIP_OK(hipSetDevice(d->device));
+  d->release_xsl();
+  d->kept_nc = 0;  // a kept evaluation cannot be completed from a freed Y
+  if (d->d_ybuf) {
+    d->sync();
+    HIP_OK(hipFree(d->d_ybuf));
+    d->d_ybuf = nullptr;
+    d->cap_ybuf = 0;
+  }
 }
 void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0) {
   static_cast<DeviceCtx*>(e)->load(x, nf, nl, nt, t0);
@@ -3415,12 +3455,6 @@ void device_synchronize(int device) {
 void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double* mu, int dens, double alpha,
                          bool need_h, double* stats) {
   static_cast<DeviceCtx*>(e)->run_eval(w, nc, mu, dens, alpha, need_h, stats);
-}
-int rccl_unique_id(char* out) {
-  ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return 1;
-  std::memcpy(out, &id, sizeof id);
-  return 0;
 }
 
 }  // namespace pcamd

@@ -62,6 +62,10 @@ class Evaluator {
   // true for a detached shard (world > 1, no communicator): every statistic is
   // this shard's partial sum, so the host driver cannot run on it alone
   virtual bool partial_sums() const { return false; }
+  // This rank failed with an error the other ranks may not see (HIP, HBM, a lost
+  // capability): end every rank's pending and later collectives with an error instead
+  // of leaving them waiting. No-op without a communicator.
+  virtual void abort_group(const std::string& why) noexcept { (void)why; }
   virtual void rowsum(double* out) = 0;
   virtual void gram(const double* mu, double* out) = 0;
   virtual void eval(const double* w, size_t nc, const double* mu, pc_density d, bool need_h,
