@@ -3218,7 +3218,10 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     if (n < 2 || n > 256) return false;
     const size_t np = n * (n + 1) / 2, npos = np;
-    const size_t mw = (np + n_cu - 1) / n_cu;
+    // matrices per workgroup fixed by the shape, not by this device's CU count: the g-sum
+    // grouping (and so every angle's bits) is then the same on any device that can hold the
+    // grid; one that cannot (fewer CUs, a partition) runs the host sweeps instead
+    const size_t mw = (np + JS_MAX_WG - 1) / JS_MAX_WG;
     const size_t G = (np + mw - 1) / mw;
     const size_t lds = (npos * mw + 4) * sizeof(double);
     if (lds > 160 * 1024 || G > (size_t)n_cu || G > (size_t)JS_MAX_WG || (n - 2) * mw > (size_t)JS_ROT_MAX * JS_THREADS)

@@ -5,7 +5,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 
 namespace pcamd {
 
@@ -29,37 +28,17 @@ inline void qr(uint32_t* x, int a, int b, int c, int d) {
   x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 7);
 }
 
-// the generated tables of rand_distr (ziggurat_tables.rs): the crates' recipe,
-// each value through its '%.18f' literal
+// the generated tables of rand_distr (ziggurat_tables.rs) as exact literals
+// (tools/gen_zig_tables.py; every entry pinned by tests/test_rust_rand.py), so no
+// value depends on the running host's libm
+#include "zig_tables.inc"
 struct ZigTables {
-  double r, x[257], f[257];
+  const double& r = ZIG_R;
+  const double* x = ZIG_X;
+  const double* f = ZIG_F;
 };
-__attribute__((optimize("fp-contract=off"))) double rs_literal(double v) {
-  char s[64];
-  std::snprintf(s, sizeof s, "%.18f", v);
-  return std::strtod(s, nullptr);
-}
-__attribute__((optimize("fp-contract=off"))) const ZigTables& zig() {
-  static ZigTables t;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    const double r = 3.6541528853610088, v = 0.00492867323399;
-    auto f = [](double x) { return std::exp(-x * x / 2.0); };
-    auto finv = [](double y) { return std::sqrt(-2.0 * std::log(y)); };
-    double xs[257];
-    xs[0] = v / f(r);
-    xs[1] = r;
-    for (int i = 2; i < 256; ++i) {
-      const double last = xs[i - 1];
-      xs[i] = finv(v / last + f(last));
-    }
-    xs[256] = 0.0;
-    t.r = rs_literal(r);
-    for (int i = 0; i <= 256; ++i) {
-      t.x[i] = rs_literal(xs[i]);
-      t.f[i] = rs_literal(f(xs[i]));
-    }
-  });
+const ZigTables& zig() {
+  static const ZigTables t;
   return t;
 }
 

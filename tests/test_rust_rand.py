@@ -37,6 +37,21 @@ def test_ziggurat_table_literals():
     assert rr.ZIG_NORM_X[256] == 0.0 and rr.ZIG_NORM_F[256] == 1.0
 
 
+def test_product_table_literals_pin_every_entry():
+    """host_rng.cpp takes the tables from zig_tables.inc (hex-float literals, no libm at
+    run time): every one of the 1 + 257 + 257 entries equals the restatement's recipe."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "picard-ica_amd", "csrc", "zig_tables.inc")).read()
+    def arr(name):
+        body = re.search(name + r"\[257\] = \{(.*?)\};", src, re.S).group(1)
+        return [float.fromhex(v) for v in re.findall(r"-?0x[0-9a-fp.+-]+", body)]
+    r = float.fromhex(re.search(r"ZIG_R = (0x[0-9a-fp.+-]+);", src).group(1))
+    assert r == rr.ZIG_NORM_R
+    assert arr("ZIG_X") == list(rr.ZIG_NORM_X) and arr("ZIG_F") == list(rr.ZIG_NORM_F)
+
+
 def test_standard_normal_moments():
     g = rr.StdRng(42)
     xs = np.array([rr.standard_normal(g) for _ in range(50000)])
