@@ -343,6 +343,13 @@ int pc_ctx_eval_loss_screen(pc_ctx* ctx, const double* w, uint64_t nc, const dou
                             double* ll_out, double* bound_out, char* err, size_t errlen);
 /* line-search screen passes since the last reset: summed HIP-event kernel ms and count */
 void pc_ctx_screen_stats(pc_ctx* ctx, double* kernel_ms, uint64_t* n_launches, int32_t reset);
+/* Exhaustive accuracy of the fp32 instructions the line-search screen evaluates its
+ * log-likelihood with (v_exp_f32, v_log_f32), measured on `device` against fp64 libm
+ * over every fp32 input of the ranges the screen uses: out[0] max relative error of 2^z
+ * on [−126, 0], out[1] max absolute error of 2^z on [−150, −126), out[2] max absolute
+ * error of log2 p on [2^-4, 1], out[3] 1 if 2^0 = 1 and log2 1 = 0 exactly. The screen's
+ * bound is built from constants these must not exceed. */
+int pc_device_check_fp32_transcendentals(int32_t device, double out[4]);
 /* hipDeviceSynchronize on `device` (bench bracketing). */
 int pc_device_synchronize(int32_t device);
 

@@ -184,6 +184,7 @@ def _load():
         "pc_ctx_last_timing": (None, [vp, d, d]),
         "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
         "pc_device_synchronize": (C.c_int, [i32]),
+        "pc_device_check_fp32_transcendentals": (C.c_int, [i32, P(C.c_double)]),
         "pc_ctx_kernel_breakdown": (None, [vp, d, P(u64), i32]),
         "pc_ctx_set_y_stage": (C.c_int, [vp, i32]),
         "pc_ctx_int8_passes": (u64, [vp]),
@@ -214,7 +215,7 @@ EXPORTED = [
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 

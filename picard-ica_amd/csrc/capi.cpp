@@ -32,6 +32,7 @@ void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double*
 int rccl_unique_id(char* out);
 void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, uint64_t* n, int reset);
 void device_synchronize(int device);
+void device_check_f32_transc(int device, double* out4);
 void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset);
 void device_ctx_set_y_stage(Evaluator* e, int mode);
 uint64_t device_ctx_int8_passes(const Evaluator* e);
@@ -487,6 +488,15 @@ int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const doubl
 
 void pc_ctx_screen_stats(pc_ctx* c, double* ms, uint64_t* n, int32_t reset) {
   device_ctx_screen_stats(c->ev.get(), ms, n, reset);
+}
+
+int pc_device_check_fp32_transcendentals(int32_t device, double out[4]) {
+  try {
+    device_check_f32_transc(device, out);
+    return PC_OK;
+  } catch (const PicardError& e) {
+    return e.code;
+  }
 }
 
 int pc_device_synchronize(int32_t device) {

@@ -222,6 +222,7 @@ struct RowAcc {
   double d = 0.0, l = 0.0, q = 0.0;  // raw Σψ′ term, raw Σℓ term, Σy²
   double p = 1.0;                    // tanh: Π (2 + em), mantissa
   int e = 0;                         //       … and its binary exponent
+  double g = 0.0;                    // tanh screen (fp32 ℓ): Σ log2 Π((1 + e^{−2α|y|})/2)
 };
 
 // e^x table for exp_n: T_j = 2^(j/32) (correctly rounded), with the high word
@@ -416,6 +417,24 @@ __device__ __forceinline__ void loss_acc4(const d4& y, double alpha, double m2a,
       }
     }
   }
+}
+
+// ℓ terms of the line-search screen for tanh in fp32 (the screen's bound covers the error):
+// Σ|y| in fp64 as the exact pass; the log term per lane and block as ONE v_log_f32 of the
+// product of the 4 factors (1 + 2^z)/2 ∈ (1/2, 1], 2^z = e^{−2α|y|} by v_exp_f32 with
+// z = fl32(|y|)·c32, c32 = fl32(−2α·log2 e). Every term vanishes at y = 0 (2^0 = 1,
+// log2 1 = 0 exactly on the hardware, checked by k_check_f32_transc), so padding is free.
+// Raw Σℓ = Σ|y| + (ln2/α)·g; finalize_row adds n·ln2/α as for the exact form.
+// Error per block and lane (4 elements, in Σℓ units), DeviceCtx::screen_f32_block_bound.
+__device__ __forceinline__ void loss_acc4_f32(const d4& y, float c32, RowAcc& a) {
+  float pf = 1.0f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a.l += fabs(y[i]);
+    const float z = (float)fabs(y[i]) * c32;
+    pf *= __builtin_fmaf(__builtin_amdgcn_exp2f(z), 0.5f, 0.5f);
+  }
+  a.g += (double)__builtin_amdgcn_logf(pf);
 }
 
 // every ≤ 32 blocks (≤ 128 factors ∈ (1, 2] since the last call: no overflow);
@@ -1979,6 +1998,46 @@ __device__ __forceinline__ double laplace_of(uint64_t st) {
 
 #include "jade_sweeps.inc"
 
+// ---------------------------------------------------------------------------
+// Exhaustive accuracy of the fp32 transcendental instructions the line-search
+// screen uses (v_exp_f32 = 2^x, v_log_f32 = log2 x), over every fp32 input of the
+// ranges the screen feeds them: the screen's rigorous bound (DeviceCtx::
+// eval_loss_screen) is built from compile-time constants that these measurements
+// must not exceed (tests/test_gpu_screen32.py). fp64 libm is the reference.
+//   out[blk][0]: max |2^z_hw − 2^z| / 2^z over z ∈ [−126, 0]
+//   out[blk][1]: max |2^z_hw − 2^z| (absolute) over z ∈ [−150, −126)
+//   out[blk][2]: max |log2_hw p − log2 p| (absolute) over p ∈ [2^-4, 1]
+//   out[blk][3]: 1 unless 2^0 ≠ 1 or log2 1 ≠ 0 (then 0)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_check_f32_transc(double* __restrict__ out) {
+  __shared__ double red[4][256];
+  double m0 = 0.0, m1 = 0.0, m2 = 0.0, ok = 1.0;
+  const uint32_t nthr = gridDim.x * blockDim.x, id = blockIdx.x * blockDim.x + threadIdx.x;
+  // z: bit patterns 0x80000000 (−0) … 0xC3160000 (−150)
+  for (uint32_t b = 0x80000000u + id; b <= 0xC3160000u; b += nthr) {
+    const float z = __uint_as_float(b);
+    const double hw = (double)__builtin_amdgcn_exp2f(z), ref = exp2((double)z);
+    if (z >= -126.0f) m0 = fmax(m0, fabs(hw - ref) / ref);
+    else m1 = fmax(m1, fabs(hw - ref));
+  }
+  // p: bit patterns of 2^-4 … 1
+  for (uint32_t b = 0x3d800000u + id; b <= 0x3f800000u; b += nthr) {
+    const float p = __uint_as_float(b);
+    m2 = fmax(m2, fabs((double)__builtin_amdgcn_logf(p) - log2((double)p)));
+  }
+  if (id == 0 && (__builtin_amdgcn_exp2f(0.0f) != 1.0f || __builtin_amdgcn_logf(1.0f) != 0.0f)) ok = 0.0;
+  red[0][threadIdx.x] = m0; red[1][threadIdx.x] = m1; red[2][threadIdx.x] = m2; red[3][threadIdx.x] = ok;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      for (int c = 0; c < 4; ++c)
+        red[c][threadIdx.x] = c == 3 ? fmin(red[c][threadIdx.x], red[c][threadIdx.x + s])
+                                     : fmax(red[c][threadIdx.x], red[c][threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) out[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+
 __global__ void k_gen_sources(double* __restrict__ S, uint64_t lds, int nf, uint64_t t_begin, uint64_t cn,
                               uint64_t seed, uint64_t jump_a, uint64_t jump_c) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -2792,7 +2851,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_wsc, sc, 128 * sizeof(double), hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
-  template <int D, bool Q, int DMAX = OZ_SLICES - 1>
+  template <int D, bool Q, int DMAX = OZ_SLICES - 1, bool F32L = false>
   void launch_loss_oz(double alpha, bool store, double* st_rows) {
     const uint64_t n_blocks = (n_local_ + 15) / 16;
     uint64_t bpw;
@@ -2801,7 +2860,8 @@ struct DeviceCtx : Evaluator {
     // never launch on a released image (callers allocate their buffers before relying on it)
     if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
     const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
-    auto kern = store ? k_eval_loss_oz<D, true, Q, DMAX> : k_eval_loss_oz<D, false, Q, DMAX>;
+    auto kern = F32L ? k_eval_loss_oz<D, false, Q, DMAX, F32L>
+                     : store ? k_eval_loss_oz<D, true, Q, DMAX> : k_eval_loss_oz<D, false, Q, DMAX>;
     lds_attr((const void*)kern, (int)lds);
     HIP_OK(hipEventRecord(ev[1], stream));
     kern<<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, alpha, bpw, n_blocks, part,
@@ -2815,6 +2875,9 @@ struct DeviceCtx : Evaluator {
     if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
   }
   uint64_t n_screen_passes_ = 0;
+  // the tanh screen evaluates ℓ in fp32 (PICARD_SCREEN_F64=1: the fp64 row terms of the
+  // exact pass, a tighter bound at a higher cost)
+  bool screen_f32_ = std::getenv("PICARD_SCREEN_F64") == nullptr;
   // Sources on the int8 digit stage (k_ystore_oz) when this context already holds the digit
   // image of the current centring: W digits uploaded, blocks b_first … of the image, Y
   // row-major (ld ldy), samples [0, n_out) of that range. The image is never built for a
@@ -2869,6 +2932,23 @@ struct DeviceCtx : Evaluator {
   // moves by at most Lip·2^(f_i−12)·B·Σ_t 2^e_t; 1e-10 of Σ_t|ℓ| covers the rounding
   // of both passes (their sums run in the same order). Ortho densities tanh / exp.
   static constexpr int OZ_SCREEN_DMAX = 4;
+  // fp32 ℓ in the tanh screen (loss_acc4_f32): hardware error constants, each at least the
+  // exhaustive measurement of pc_device_check_fp32_transcendentals on MI355X (the -m gpu
+  // test fails if a device exceeds them): v_exp_f32 relative on [−126, 0], absolute below;
+  // v_log_f32 absolute on [2^-4, 1] (the product of 4 factors in [1/2, 1]). Measured:
+  // 1.42·2^-24 and 8.0·2^-24 on [2^-6, 1] (tests/test_gpu_screen32.py)
+  static constexpr double SCREEN_EXP2_REL = 0x1p-23, SCREEN_EXP2_TINY = 0x1p-124, SCREEN_LOG2_ABS = 0x1p-21;
+  // Bound (Σℓ units) on |Σ of one lane-block's 4 fp32 ℓ log terms − the exact ones|:
+  //   z = fl32(|y|)·c32 is within 3.0000002·2^-24·|z*| of z* = −2α|y|·log2 e, so
+  //   |2^z − 2^z*| ≤ 2^z*·|z*|·3.0003·2^-24·ln2 ≤ 1.1038·2^-24 (max_z |z|2^z = 1/(e·ln2));
+  //   v_exp_f32 adds ≤ E_rel·2^z/(1 + 2^z) ≤ E_rel/2 (in (1+e) relative terms), or E_tiny;
+  //   fl32((1+e)/2) and the 3 products round by 2^-24 each; v_log_f32 adds E_log;
+  //   d log2 = d(1+e)/((1+e)·ln2), and the log2 sum enters Σℓ times ln2/α.
+  static double screen_f32_block_bound(double alpha) {
+    const double u = 0x1p-24;
+    const double per_elem = 1.1038 * u + 0.50005 * SCREEN_EXP2_REL + u + SCREEN_EXP2_TINY;
+    return 1.001 * (4.0 * per_elem + 3.0 * u + fm::LN2 * SCREEN_LOG2_ABS) / alpha;
+  }
   bool eval_loss_screen(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
                         double* bound_out) override {
     if (y_stage_ != 0 || !oz_shape(nc) || !(d.alpha > 0.0) || (d.kind != DENS_TANH && d.kind != DENS_EXP))
@@ -2891,7 +2971,9 @@ struct DeviceCtx : Evaluator {
     d_wsl_ready_ = true;
     kept_nc_pending = nc;
     HIP_OK(hipEventRecord(ev[0], stream));
-    if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
+    const bool f32l = d.kind == DENS_TANH && screen_f32_;
+    if (f32l) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX, true>(d.alpha, false, st_rows);
+    else if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
     else launch_loss_oz<DENS_EXP, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
     // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
     double bsum = 0.0;
@@ -2916,6 +2998,8 @@ struct DeviceCtx : Evaluator {
       int e = 0;
       if (mx > 0.0) (void)std::frexp(mx, &e);
       bnd[i] = std::ldexp(tail, e - 12) * (1.0 + 1e-12);
+      // fp32 ℓ: 4 lane-blocks of 4 samples per 16-sample block of this row (padding included)
+      if (f32l) bnd[i] += (double)(ldx / 4) * screen_f32_block_bound(d.alpha);
     }
     HIP_OK(hipMemcpyAsync(st_rows + nc, bnd.data(), nc * sizeof(double), hipMemcpyHostToDevice, stream));
     allreduce(st_rows, 2 * nc, "screen");
@@ -3450,6 +3534,23 @@ void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset) {
   *ms = d->sum_screen_ms;
   *n = d->n_screen;
   if (reset) { d->sum_screen_ms = 0; d->n_screen = 0; }
+}
+void device_check_f32_transc(int device, double* out4) {
+  HIP_OK(hipSetDevice(device));
+  const int nblk = 2048;
+  double* d = nullptr;
+  HIP_OK(hipMalloc(&d, nblk * 4 * sizeof(double)));
+  k_check_f32_transc<<<nblk, 256>>>(d);
+  HIP_OK(hipGetLastError());
+  std::vector<double> h(nblk * 4);
+  HIP_OK(hipMemcpy(h.data(), d, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  out4[0] = out4[1] = out4[2] = 0.0;
+  out4[3] = 1.0;
+  for (int b = 0; b < nblk; ++b) {
+    for (int c = 0; c < 3; ++c) out4[c] = std::max(out4[c], h[b * 4 + c]);
+    out4[3] = std::min(out4[3], h[b * 4 + 3]);
+  }
 }
 void device_synchronize(int device) {
   HIP_OK(hipSetDevice(device));
