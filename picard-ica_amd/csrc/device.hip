@@ -2925,13 +2925,16 @@ struct DeviceCtx : Evaluator {
   }
 
   // The orthogonal line-search screen (Evaluator::eval_loss_screen): the loss-only
-  // pass on diagonals D ≤ 4 of the int8 digit stage (15 digit products instead of
-  // 28). The exact stage's y differs from it by 2^(f_i+e_t−12)·Σ_{D=5,6} 256^−D·P_D,
+  // pass on diagonals D ≤ DMAX of the int8 digit stage (DMAX = 3: 10 digit products
+  // instead of 28). The exact stage's y differs from it by 2^(f_i+e_t−12)·Σ_{D>DMAX} 256^−D·P_D,
   // |P_D| ≤ nf·Σ_{a+b=D} |d_a|max·|d_b|max (|d_0| ≤ 65, |d_a| ≤ 128), so with ℓ
   // Lipschitz in y (tanh: |ℓ′| = |tanh αy| ≤ 1; exp: |ℓ′| ≤ 1/√(αe)) each row's Σℓ
   // moves by at most Lip·2^(f_i−12)·B·Σ_t 2^e_t; 1e-10 of Σ_t|ℓ| covers the rounding
   // of both passes (their sums run in the same order). Ortho densities tanh / exp.
-  static constexpr int OZ_SCREEN_DMAX = 4;
+  // diagonals the screen keeps: D ≤ 3 (10 digit products, 4 planes) by default; its bound is
+  // then ≈ 7× the D ≤ 4 screen's, which still decides every C3 rejection
+  // (PICARD_SCREEN_DMAX=4: 15 products, 5 planes)
+  int screen_dmax_ = std::getenv("PICARD_SCREEN_DMAX") && std::atoi(std::getenv("PICARD_SCREEN_DMAX")) == 4 ? 4 : 3;
   // fp32 ℓ in the tanh screen (loss_acc4_f32): hardware error constants, each at least the
   // exhaustive measurement of pc_device_check_fp32_transcendentals on MI355X (the -m gpu
   // test fails if a device exceeds them): v_exp_f32 relative on [−126, 0], absolute below;
@@ -2951,6 +2954,15 @@ struct DeviceCtx : Evaluator {
   }
   bool eval_loss_screen(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
                         double* bound_out) override {
+    return screen_at(screen_dmax_, w, nc, mu, d, ll_out, bound_out);
+  }
+  // the finer screen: D ≤ 4 (only when the default is coarser)
+  bool eval_loss_screen_fine(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+                             double* bound_out) override {
+    return screen_dmax_ < 4 && screen_at(4, w, nc, mu, d, ll_out, bound_out);
+  }
+  bool screen_at(int dmax, const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+                 double* bound_out) {
     if (y_stage_ != 0 || !oz_shape(nc) || !(d.alpha > 0.0) || (d.kind != DENS_TANH && d.kind != DENS_EXP))
       return false;
     HIP_OK(hipSetDevice(device));
@@ -2972,12 +2984,15 @@ struct DeviceCtx : Evaluator {
     kept_nc_pending = nc;
     HIP_OK(hipEventRecord(ev[0], stream));
     const bool f32l = d.kind == DENS_TANH && screen_f32_;
-    if (f32l) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX, true>(d.alpha, false, st_rows);
-    else if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
-    else launch_loss_oz<DENS_EXP, false, OZ_SCREEN_DMAX>(d.alpha, false, st_rows);
+    if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true>(d.alpha, false, st_rows);
+    else if (f32l) launch_loss_oz<DENS_TANH, false, 4, true>(d.alpha, false, st_rows);
+    else if (d.kind == DENS_TANH && dmax == 3) launch_loss_oz<DENS_TANH, false, 3>(d.alpha, false, st_rows);
+    else if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, 4>(d.alpha, false, st_rows);
+    else if (dmax == 3) launch_loss_oz<DENS_EXP, false, 3>(d.alpha, false, st_rows);
+    else launch_loss_oz<DENS_EXP, false, 4>(d.alpha, false, st_rows);
     // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
     double bsum = 0.0;
-    for (int dd = OZ_SCREEN_DMAX + 1; dd <= 2 * (OZ_SLICES - 1); ++dd) {
+    for (int dd = dmax + 1; dd <= 2 * (OZ_SLICES - 1); ++dd) {
       double pm = 0.0;
       for (int a = 0; a < OZ_SLICES; ++a) {
         const int b = dd - a;

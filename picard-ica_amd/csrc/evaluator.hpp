@@ -97,6 +97,13 @@ class Evaluator {
     (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
     return false;
   }
+  // The same on a finer (slower, tighter) approximation, for tries the default screen left
+  // undecided although its estimate lies above the current loss. false = none.
+  virtual bool eval_loss_screen_fine(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+                                     double* bound_out) {
+    (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
+    return false;
+  }
   // Non-ortho line search: Σℓ and Σy² of Y_j = (W + α_j·Z)·(X−μ) for every α_j
   // in one pass (ll_out, y2_out: [na][nc]). false = not supported here.
   virtual bool eval_loss_multi(const double* w, const double* z, size_t nc, const double* mu, pc_density d,

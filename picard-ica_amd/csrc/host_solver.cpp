@@ -596,6 +596,24 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         if (trace_)
           std::fprintf(stderr, "[picard-screen] try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", k + 1, alpha,
                        lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact");
+        // undecided, but the estimate lies above the current loss (a likely rejection): the
+        // finer screen first, when the evaluator has one, before the full pass. Its inputs
+        // are the reduced statistics, so every rank takes the same branch.
+        if (!rejected && lo + eb > current_loss_ &&
+            ev_->eval_loss_screen_fine(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(),
+                                       bnd.data())) {
+          ++screen_passes_;
+          lo = 0.0;
+          eb = 0.0;
+          for (size_t i = 0; i < n; ++i) {
+            lo += (signs_[i] * ll[i] - std::fabs(signs_[i]) * bnd[i]) / (double)T_;
+            eb += std::fabs(signs_[i]) * bnd[i] / (double)T_;
+          }
+          rejected = !(lo < current_loss_);
+          if (trace_)
+            std::fprintf(stderr, "[picard-screen] fine try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", k + 1,
+                         alpha, lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact");
+        }
       }
       if (rejected) {
         if (first_policy) first_n_[first_full_ ? 1 : 0] += 1.0;

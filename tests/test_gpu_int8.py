@@ -218,7 +218,7 @@ def test_int8_gram_stays_fp64(pa, rng):
 def test_screen_bound_holds(pa, rng, n, dens):
     """The line-search screen's bound covers the exact pass: |Σℓ_exact − Σℓ_screen| ≤ bound
     for every row, over W of very different scales; and it is tight enough to decide
-    (bound ≤ 1e-6 of Σ|ℓ|)."""
+    (tanh: bound ≤ 1e-4 of Σ|ℓ| with the default D ≤ 3 screen and its fp32 log-likelihood)."""
     x = laplace_mix(rng, n, 20011)
     x[:, 5] *= 1e3  # one loud sample: its exponent dominates its own column only
     ctx = pa.DeviceContext(0)
@@ -235,7 +235,7 @@ def test_screen_bound_holds(pa, rng, n, dens):
         assert np.all(err <= bnd), (scale, np.max(err / bnd))
         assert np.all(bnd >= 0)
         if dens[0] == "tanh":
-            assert np.max(bnd / np.abs(lo["ll"])) <= 1e-6, (scale, np.max(bnd / np.abs(lo["ll"])))
+            assert np.max(bnd / np.abs(lo["ll"])) <= 1e-4, (scale, np.max(bnd / np.abs(lo["ll"])))
     _, ns = ctx.screen_stats()
     assert ns == 4
 

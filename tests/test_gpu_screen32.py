@@ -5,8 +5,9 @@ constants: the relative error of v_exp_f32 on [−126, 0], its absolute error be
 and the absolute error of v_log_f32 on [2^-4, 1]. They are checked here
 exhaustively — every fp32 input of those ranges against fp64 libm, on this device —
 so the bound is rigorous on the hardware the tests run on. Then: the bound covers
-the exact pass on hard inputs, it still decides (≤ 1e-6 of Σℓ), and the fp64-ℓ
-screen (PICARD_SCREEN_F64=1) agrees within both bounds."""
+the exact pass on hard inputs, it stays small (≤ 1e-4 of Σℓ on the default D ≤ 3
+digit diagonals, 1e-5 on D ≤ 4; whether it decides is measured on C3), and the fp64-ℓ screen (PICARD_SCREEN_F64=1) agrees within
+both bounds. Both screen depths (PICARD_SCREEN_DMAX = 3, 4) are covered."""
 import numpy as np
 import pytest
 
@@ -34,7 +35,9 @@ def _laplace_mix(rng, n, t):
 
 @pytest.mark.parametrize("n", [72, 128])
 @pytest.mark.parametrize("alpha", [1.0, 0.5, 2.0])
-def test_f32_screen_bound_covers_exact(pa, n, alpha, monkeypatch):
+@pytest.mark.parametrize("dmax", ["3", "4"])
+def test_f32_screen_bound_covers_exact(pa, n, alpha, dmax, monkeypatch):
+    monkeypatch.setenv("PICARD_SCREEN_DMAX", dmax)
     rng = np.random.default_rng(n)
     x = _laplace_mix(rng, n, 30011)
     x[:, 7] *= 1e4  # one loud sample
@@ -58,4 +61,5 @@ def test_f32_screen_bound_covers_exact(pa, n, alpha, monkeypatch):
         assert np.all(np.abs(exact - ll32) <= b32), (scale, np.max(np.abs(exact - ll32) / b32))
         assert np.all(np.abs(exact - ll64) <= b64)
         assert np.all(b32 >= b64)  # the fp32 bound adds to the digit tail
-        assert np.max(b32 / np.abs(exact)) <= 1e-6, (scale, np.max(b32 / np.abs(exact)))
+        tight = 1e-4 if dmax == "3" else 1e-5  # the dropped digit diagonals dominate the bound
+        assert np.max(b32 / np.abs(exact)) <= tight, (scale, np.max(b32 / np.abs(exact)))

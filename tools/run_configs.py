@@ -54,7 +54,21 @@ def run(name, oracle=False, max_iter=None):
     print(json.dumps(out), flush=True)
 
 
+def dump_maps_at_exit(path):
+    """--maps=PATH: write /proc/self/maps when the interpreter finalises (to map the PCs of
+    a crash in exit() to libraries and offsets afterwards)."""
+    import atexit
+
+    def dump():
+        with open("/proc/self/maps") as f, open(path, "w") as g:
+            g.write(f.read())
+    atexit.register(dump)
+
+
 if __name__ == "__main__":
+    for a in sys.argv[1:]:
+        if a.startswith("--maps="):
+            dump_maps_at_exit(a.split("=", 1)[1])
     want_oracle = "--oracle" in sys.argv
     mi = [int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--max-iter=")]
     for name in [a for a in sys.argv[1:] if not a.startswith("--")]:
