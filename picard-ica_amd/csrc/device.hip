@@ -483,6 +483,8 @@ __host__ __device__ inline double finalize_row(int dens, double alpha, double n,
 // density interleave widths (register budget: fused 256 VGPRs, split kernels 128)
 constexpr int FUSED_NW = 2, LOSS_NW = 1, FROMY_NW = 1;
 
+#include "ozaki.inc"  // the int8-digit Y stage (k_eval_fused<4, …, OZ> uses it too)
+
 // ---------------------------------------------------------------------------
 // The fused pass. NB = 16-row blocks of Y (nc ≤ 16·NB), 8 waves.
 // Block = TB = 16·(8/NB) samples; each wave owns one 16×16 Yᵀ tile of it.
@@ -514,11 +516,18 @@ __host__ __device__ inline size_t fused_partial_stride(int ncp, bool need_h) {
 // indices instead of branches (the last iteration is peeled); the row sums
 // need no validity masks (RowAcc).
 // X rows are padded to ldx ≡ 0 (mod 128) so a TB-sample tile never crosses a row end.
-template <int NB, bool NEED_H, int DENS, bool NEED_Q>
+// OZ (NB = 4, nf ≤ 64, centred resident X): the Y stage runs on the int8 digit image
+// (ozaki.inc: oz_ystage + oz_combine on 1 k-step, the arithmetic of k_eval_loss_oz<…, 4>,
+// so the loss-only try and this pass give identical bits); the two 7-KiB digit images
+// and the 32 scales of a block are staged by LDS-DMA in place of X.
+template <int NB, bool NEED_H, int DENS, bool NEED_Q, bool OZ = false>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int nf,
              const double* __restrict__ Wp, const double* __restrict__ mu, double alpha,
-             uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials) {
+             uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials,
+             const uint8_t* __restrict__ xsl = nullptr, const double* __restrict__ xsc = nullptr,
+             const uint8_t* __restrict__ wsl_g = nullptr, const double* __restrict__ wsc = nullptr) {
+  static_assert(!OZ || NB == 4, "int8 Y stage of k_eval_fused: NB = 4");
   using S = FusedShape<NB>;
   constexpr int TS = S::TS, TB = S::TB, NCP = S::NCP, KKW = S::KKW, GI = S::GI, GJ = S::GJ;
   constexpr int NFP = 16 * NB;       // K of the Y stage, padded (zero X rows / zero W columns)
@@ -539,9 +548,18 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   double* xs0 = smem;             // [2][TS][NFP][16]
   double* img0 = smem + 2 * XS;   // [2][NIMG][KK][NB][64]
 
-  double wf[KS];
+  double wf[OZ ? 1 : KS];
+  v4i wsl[OZ ? OZ_SLICES : 1][1];
+  double rsc = 0.0;
+  if constexpr (OZ) {
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) wf[ks] = Wp[(yi * 16 + lr) * NFP + 4 * ks + lk];
+    for (int a = 0; a < OZ_SLICES; ++a)
+      wsl[a][0] = *(const v4i*)(wsl_g + (size_t)(((yi * OZ_SLICES + a) * 2 + 0) * 64 + lane) * 16);
+    rsc = wsc[yi * 16 + lr];
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) wf[ks] = Wp[(yi * 16 + lr) * NFP + 4 * ks + lk];
+  }
 
   int gi0, gj0, kk0;
   if constexpr (NB == 8) { gi0 = (wave >> 2) * 4; gj0 = (wave & 3) * 2; kk0 = 0; }
@@ -605,12 +623,38 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
   // Y stage: Yᵀ tile (16 samples × 16 rows) = Xᵀ·Wᵀ over NFP as ONE accumulation
   // chain (back-to-back dependent fp64 MFMAs issue at full rate on gfx950:
   // tools/microbench/mfma_chain.hip), in the same order as k_eval_loss
+  constexpr int OZT = oz_block_bytes<1>();  // OZ: one 16-sample sub-block's digit image
+  static_assert(!OZ || 2 * OZT + 256 <= XS * (int)sizeof(double), "digit images fit the X tile");
   auto y_stage = [&](const double* xs) {
-    d4 ya = d4{0, 0, 0, 0};
-    const double* xrow = xs + (yts * NFP + lk) * 16 + lr;
+    if constexpr (OZ) {
+      v4i acc[OZ_SLICES];
+      const uint8_t* tile = (const uint8_t*)xs + yts * OZT;
+      oz_ystage<OZ_SLICES - 1, 1>(tile, lane, wsl, acc);
+      const double* scd = (const double*)((const uint8_t*)xs + 2 * OZT) + yts * 16;
+      const double x4[4] = {scd[lk], scd[lk + 4], scd[lk + 8], scd[lk + 12]};
+      return oz_combine(acc, rsc, x4);
+    } else {
+      d4 ya = d4{0, 0, 0, 0};
+      const double* xrow = xs + (yts * NFP + lk) * 16 + lr;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
-    return ya;
+      for (int ks = 0; ks < KS; ++ks) ya = mfma(xrow[(4 * ks) * 16], wf[ks], ya);
+      return ya;
+    }
+  };
+  // OZ: block b's 2 × 7 digit planes (1 KiB each) and its 32 scales → xs by LDS-DMA; wave w
+  // moves items w and w + 8 of the 15 (item 14: the scales, 4 B per lane)
+  auto stage_oz = [&](uint64_t b, double* xs) {
+    uint8_t* dst = (uint8_t*)xs;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = wave + 8 * u;
+      if (it < 14)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(xsl + (2 * b) * OZT + it * 1024 + lane * 16),
+                                         (lds_vptr)(dst + it * 1024), 16, 0, 0);
+      else if (it == 14)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)((const uint32_t*)(xsc + b * 32) + lane),
+                                         (lds_vptr)(dst + 2 * OZT), 4, 0, 0);
+    }
   };
   // density on the tile, row terms, hand-off of the ψ / y (/ ψ′) fragments
   auto elementwise = [&](const d4& yv, double* img) {
@@ -649,7 +693,39 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
     }
   };
 
-  if (b_begin < b_end) {
+  if (OZ && b_begin < b_end) {  // the same schedule with the digit images staged by DMA
+    auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
+    stage_oz(b_begin, xs0);
+    __syncthreads();  // (also waits for this wave's LDS-DMA)
+    elementwise(y_stage(xs0), img0);
+    stage_oz(clampb(b_begin + 1), xs0 + XS);
+    __syncthreads();
+    // iteration b: block b+2 → xs[cur] (block b was consumed in iteration b−1) ‖ Y stage of
+    // b+1 ‖ G stage of b
+    auto iter = [&](uint64_t b, int cur) {
+      stage_oz(clampb(b + 2), xs0 + cur * XS);
+      const d4 yv = y_stage(xs0 + (cur ^ 1) * XS);     // block b+1
+      g_stage(img0 + cur * NIMG * S::FRAGS);           // block b
+      elementwise(yv, img0 + (cur ^ 1) * NIMG * S::FRAGS);
+      __syncthreads();
+    };
+    uint64_t b = b_begin;
+    while (b + 1 < b_last) {
+      const uint64_t lim = b + RENORM_BLOCKS < b_last ? b + RENORM_BLOCKS : b_last;
+      for (; b + 1 < lim; b += 2) {
+        iter(b, 0);
+        iter(b + 1, 1);
+      }
+      acc_renorm<DENS>(racc);
+    }
+    int cur = 0;
+    if (b < b_last) {
+      iter(b, 0);
+      cur = 1;
+    }
+    g_stage(img0 + cur * NIMG * S::FRAGS);  // block b_last
+    __syncthreads();
+  } else if (b_begin < b_end) {
     auto clampb = [&](uint64_t b) { return b < b_last ? b : b_last; };
     // prologue: X(b0) → xs[0]; Y + density of b0 → img[0]; X(b0+1) → xs[1]; X(b0+2) → preA
     load_x(b_begin, preA);
@@ -765,7 +841,6 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 // of barriers. Same block partition, G-tile map, k order, lane map and row-term
 // formulas as k_eval_fused<8> / k_eval_loss<8> / k_eval_fromy<8>: identical sums.
 // ---------------------------------------------------------------------------
-#include "ozaki.inc"
 #include "fused_ws.inc"
 
 // ---------------------------------------------------------------------------
@@ -2405,18 +2480,23 @@ struct DeviceCtx : Evaluator {
     const bool ws = NB == 8 && !H;
     // (after the partial buffer: an allocation that released the digit image falls back to
     // the fp64 Y stage, which issues the same collectives)
-    const bool oz = ws && D != DENS_LINEAR && dmu == nullptr && oz_fused_ready_ && xsl_valid_;
+    const bool oz_ok = D != DENS_LINEAR && dmu == nullptr && oz_fused_ready_ && xsl_valid_;
+    const bool oz = ws && oz_ok;
+    // NB = 4 without H, nf ≤ 64: k_eval_fused<4> on the int8-digit Y stage
+    constexpr bool OZ4 = NB == 4 && !H && D != DENS_LINEAR;
+    const bool oz4 = OZ4 && oz_ok && oz_kso() == 1;
     auto kws = oz ? k_eval_fused_ws<D, Q, true> : k_eval_fused_ws<D, Q, false>;
-    auto kfu = k_eval_fused<NB, H, D, Q>;
+    auto kfu = oz4 ? k_eval_fused<NB, H, D, Q, OZ4> : k_eval_fused<NB, H, D, Q, false>;
     lds_attr(ws ? (const void*)kws : (const void*)kfu, 160 * 1024 - EXP_TAB_BYTES);
     HIP_OK(hipEventRecord(ev[1], stream));
     if (ws)
       kws<<<nwg, WS_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part, d_xsl, d_xsc,
                                            d_wsl, d_wsc);
     else
-      kfu<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part);
+      kfu<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part, d_xsl,
+                                               d_xsc, d_wsl, d_wsc);
     HIP_OK(hipGetLastError());
-    if (oz) ++n_int8_passes_;
+    if (oz || oz4) ++n_int8_passes_;
     HIP_OK(hipEventRecord(ev[2], stream));
     const size_t total = EvalStats::size(nc, H);
     k_reduce<<<(total + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D, alpha,
@@ -2472,7 +2552,7 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipMemcpyAsync(d_w, wp, nwp * sizeof(double), hipMemcpyHostToDevice, stream));
       pin_release(pin_w_);
       oz_fused_ready_ = false;
-      if (dmu == nullptr && !need_h && dens != DENS_LINEAR && oz_shape(nc) && ensure_xsl()) {
+      if (dmu == nullptr && !need_h && dens != DENS_LINEAR && oz_any(nc) && ensure_xsl()) {
         upload_wsl(w, nc);
         oz_fused_ready_ = true;
       }
@@ -2783,6 +2863,11 @@ struct DeviceCtx : Evaluator {
   }
   // the shapes the i8 loss kernel covers: 64 < nc ≤ 128, nf ≤ 128, centred X
   bool oz_shape(size_t nc) const { return y_stage_ != 1 && pick_nb(nc) == 8 && nf <= 128 && nf > 0; }
+  // … and the NB = 4 forms: 32 < nc ≤ 64 with nf ≤ 64 (a 1-k-step image)
+  bool oz4_shape(size_t nc) const { return y_stage_ != 1 && pick_nb(nc) == 4 && nf <= 64 && nf > 0; }
+  bool oz_any(size_t nc) const { return oz_shape(nc) || oz4_shape(nc); }
+  int oz_kso() const { return nf <= 64 ? 1 : 2; }  // k-steps of the resident X's digit image
+  size_t oz_bb() const { return oz_kso() == 1 ? (size_t)oz_block_bytes<1>() : (size_t)oz_block_bytes<2>(); }
   bool ensure_xsl() {
     if (xsl_valid_) return true;
     if (xsl_failed_) return false;
@@ -2791,7 +2876,7 @@ struct DeviceCtx : Evaluator {
     ensure(d_shift_part, cap_shift_part, (size_t)nwg_e + 1);
     if (xsl_failed_) return false;
     const uint64_t n_blocks = ldx / 16;
-    const size_t need = (size_t)n_blocks * OZ_BLOCK_BYTES;
+    const size_t need = (size_t)n_blocks * oz_bb();
     if (need > cap_xsl) {
       size_t fr = 0, tot = 0;
       HIP_OK(hipMemGetInfo(&fr, &tot));
@@ -2809,7 +2894,8 @@ struct DeviceCtx : Evaluator {
       cap_xsl = need;
     }
     const unsigned grid = (unsigned)std::min<uint64_t>(n_blocks, (uint64_t)n_cu * 16);
-    k_slice_x<<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
+    if (oz_kso() == 1) k_slice_x<1><<<grid, 64, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
+    else k_slice_x<2><<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     HIP_OK(hipGetLastError());
     {  // Σ_t 2^e_t of this shard (padding included: it only loosens the screen's bound)
       const int nwg = nwg_e;
@@ -2851,17 +2937,21 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_wsc, sc, 128 * sizeof(double), hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
-  template <int D, bool Q, int DMAX = OZ_SLICES - 1, bool F32L = false>
+  // NB = 8 (64 < nc ≤ 128) or NB = 4 (32 < nc ≤ 64, nf ≤ 64; partition in 32-sample blocks,
+  // that of k_eval_fused<4> / k_eval_loss<4>)
+  template <int D, bool Q, int DMAX = OZ_SLICES - 1, bool F32L = false, int NB = 8>
   void launch_loss_oz(double alpha, bool store, double* st_rows) {
-    const uint64_t n_blocks = (n_local_ + 15) / 16;
+    constexpr int NCP = 16 * NB, KSO = NB == 8 ? 2 : 1;
+    const uint64_t n_blocks = NB == 8 ? (n_local_ + 15) / 16 : (n_local_ + 31) / 32;
     uint64_t bpw;
     const int nwg = partition(n_blocks, &bpw);
-    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * 128);
+    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
     // never launch on a released image (callers allocate their buffers before relying on it)
     if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
-    const size_t lds = (size_t)2 * 2 * (OZ_BLOCK_BYTES + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
-    auto kern = F32L ? k_eval_loss_oz<D, false, Q, DMAX, F32L>
-                     : store ? k_eval_loss_oz<D, true, Q, DMAX> : k_eval_loss_oz<D, false, Q, DMAX>;
+    if (oz_kso() != KSO) throw computation_error("int8 digit image of another layout");
+    const size_t lds = (size_t)2 * 2 * (oz_block_bytes<KSO>() + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
+    auto kern = F32L ? k_eval_loss_oz<D, false, Q, DMAX, F32L, NB>
+                     : store ? k_eval_loss_oz<D, true, Q, DMAX, false, NB> : k_eval_loss_oz<D, false, Q, DMAX, false, NB>;
     lds_attr((const void*)kern, (int)lds);
     HIP_OK(hipEventRecord(ev[1], stream));
     kern<<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, alpha, bpw, n_blocks, part,
@@ -2869,7 +2959,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(ev[2], stream));
     k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
-        part, nwg, 2 * 128, 0, 128, (int)kept_nc_pending, 2, st_rows, D, alpha, (double)n_local_, 1);
+        part, nwg, 2 * NCP, 0, NCP, (int)kept_nc_pending, 2, st_rows, D, alpha, (double)n_local_, 1);
     HIP_OK(hipGetLastError());
     ++n_int8_passes_;
     if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
@@ -2963,15 +3053,16 @@ struct DeviceCtx : Evaluator {
   }
   bool screen_at(int dmax, const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
                  double* bound_out) {
-    if (y_stage_ != 0 || !oz_shape(nc) || !(d.alpha > 0.0) || (d.kind != DENS_TANH && d.kind != DENS_EXP))
+    if (y_stage_ != 0 || !oz_any(nc) || !(d.alpha > 0.0) || (d.kind != DENS_TANH && d.kind != DENS_EXP))
       return false;
+    const bool nb4 = oz4_shape(nc);
     HIP_OK(hipSetDevice(device));
     const double* dmu = resident_mu(mu);
     double* st_rows = ensure(d_stats, cap_stats, 2 * nc);
     {  // the pass buffers before the image is relied on (an allocation may release it)
       uint64_t bpw0;
-      const int nwg0 = partition((n_local_ + 15) / 16, &bpw0);
-      ensure(d_part, cap_part, (size_t)nwg0 * 2 * 128);
+      const int nwg0 = partition(nb4 ? (n_local_ + 31) / 32 : (n_local_ + 15) / 16, &bpw0);
+      ensure(d_part, cap_part, (size_t)nwg0 * 2 * (nb4 ? 64 : 128));
     }
     bool ok = dmu == nullptr && ensure_xsl();
     // With a communicator every rank must take the same branch (a screen and a full pass
@@ -2984,12 +3075,8 @@ struct DeviceCtx : Evaluator {
     kept_nc_pending = nc;
     HIP_OK(hipEventRecord(ev[0], stream));
     const bool f32l = d.kind == DENS_TANH && screen_f32_;
-    if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true>(d.alpha, false, st_rows);
-    else if (f32l) launch_loss_oz<DENS_TANH, false, 4, true>(d.alpha, false, st_rows);
-    else if (d.kind == DENS_TANH && dmax == 3) launch_loss_oz<DENS_TANH, false, 3>(d.alpha, false, st_rows);
-    else if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, 4>(d.alpha, false, st_rows);
-    else if (dmax == 3) launch_loss_oz<DENS_EXP, false, 3>(d.alpha, false, st_rows);
-    else launch_loss_oz<DENS_EXP, false, 4>(d.alpha, false, st_rows);
+    if (nb4) screen_launch<4>(d, dmax, f32l, st_rows);
+    else screen_launch<8>(d, dmax, f32l, st_rows);
     // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
     double bsum = 0.0;
     for (int dd = dmax + 1; dd <= 2 * (OZ_SLICES - 1); ++dd) {
@@ -3031,17 +3118,27 @@ struct DeviceCtx : Evaluator {
     return true;
   }
 
+  template <int NB>
+  void screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
+    if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);
+    else if (f32l) launch_loss_oz<DENS_TANH, false, 4, true, NB>(d.alpha, false, st_rows);
+    else if (d.kind == DENS_TANH && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, false, NB>(d.alpha, false, st_rows);
+    else if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, 4, false, NB>(d.alpha, false, st_rows);
+    else if (dmax == 3) launch_loss_oz<DENS_EXP, false, 3, false, NB>(d.alpha, false, st_rows);
+    else launch_loss_oz<DENS_EXP, false, 4, false, NB>(d.alpha, false, st_rows);
+  }
+
   template <int NB, int D, bool Q>
   void launch_loss(const double* dmu, double alpha, bool store, double* st_rows) {
     using S = FusedShape<NB>;
     const uint64_t n_blocks = (n_local_ + S::TB - 1) / S::TB;
-    if constexpr (NB == 8) {
-      if (dmu == nullptr && oz_shape(kept_nc_pending) && d_wsl_ready_) {
+    if constexpr (NB == 8 || NB == 4) {
+      if (dmu == nullptr && (NB == 8 ? oz_shape(kept_nc_pending) : oz4_shape(kept_nc_pending)) && d_wsl_ready_) {
         uint64_t bpw0;
         const int nwg0 = partition(n_blocks, &bpw0);
-        ensure(d_part, cap_part, (size_t)nwg0 * 2 * 128);  // may release an unpinned image …
+        ensure(d_part, cap_part, (size_t)nwg0 * 2 * S::NCP);  // may release an unpinned image …
         if (xsl_valid_) {  // … then the fp64 stage below runs (same collectives)
-          launch_loss_oz<D, Q>(alpha, store, st_rows);
+          launch_loss_oz<D, Q, OZ_SLICES - 1, false, NB>(alpha, store, st_rows);
           return;
         }
       }
@@ -3174,7 +3271,9 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_w, wp.data(), wp.size() * sizeof(double), hipMemcpyHostToDevice, stream));
     kept_nc_pending = nc;
     d_wsl_ready_ = false;
-    if (dmu == nullptr && oz_shape(nc) && ensure_xsl()) {
+    // the int8 stage only where the fused pass at this W runs it too (no H): a try's
+    // loss-only pass and its full evaluation must give the same bits
+    if (dmu == nullptr && oz_any(nc) && !need_h && ensure_xsl()) {
       upload_wsl(w, nc);
       d_wsl_ready_ = true;
     }

@@ -1,7 +1,8 @@
 """GPU parity of the int8-slice Y stage (ozaki.inc) against the CPU oracle.
 
 The loss-only line-search pass and the fused pass at 64 < nc ≤ 128, n_features ≤ 128
-(no H) form Y = W·(X − μ)
+(NB = 8: k_eval_loss_oz, k_eval_fused_ws) and at 32 < nc ≤ 64, n_features ≤ 64 (NB = 4:
+k_eval_loss_oz<…, 4>, k_eval_fused<4, …, OZ>), no H, form Y = W·(X − μ)
 from exact int8 digits (7 radix-256 digits per value of X and of W, exact int32 diagonal sums, fp64
 combine). Tolerances: the statistics against the fp64 oracle at the file-wide 1e-12
 relative bound of test_gpu_parity.py; against the context's own fp64 Y stage
@@ -40,7 +41,7 @@ def loss_only(ctx, w, mu, d, need_y2=True):
     return lo, kept, done
 
 
-@pytest.mark.parametrize("n", [65, 100, 128])
+@pytest.mark.parametrize("n", [40, 64, 65, 100, 128])
 @pytest.mark.parametrize("dens", DENSITIES)
 def test_int8_loss_vs_oracle(pa, po, rng, n, dens):
     t = 5003  # ragged: the last 16-sample block is partly padding
@@ -58,7 +59,7 @@ def test_int8_loss_vs_oracle(pa, po, rng, n, dens):
         assert rel_err(lo[k], want[k]) <= TOL, (k, rel_err(lo[k], want[k]))
 
 
-@pytest.mark.parametrize("nc,nf", [(128, 128), (80, 128), (72, 100), (65, 65)])
+@pytest.mark.parametrize("nc,nf", [(128, 128), (80, 128), (72, 100), (65, 65), (64, 64), (40, 64), (48, 60)])
 def test_int8_vs_f64_stage(pa, rng, nc, nf):
     """Same context, same W: the int8 stage against the fp64 MFMA stage."""
     x = laplace_mix(rng, nf, 20011)
@@ -158,7 +159,7 @@ def test_int8_fit_matches_f64_fit(pa, rng):
     assert np.max(np.abs(r.unmixing - r64.unmixing)) <= 1e-6
 
 
-@pytest.mark.parametrize("n", [100, 128])
+@pytest.mark.parametrize("n", [40, 64, 100, 128])
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
 @pytest.mark.parametrize("need_y2", [False, True])
 def test_int8_split_eval_bit_identical(pa, rng, n, dens, need_y2):
@@ -179,7 +180,7 @@ def test_int8_split_eval_bit_identical(pa, rng, n, dens, need_y2):
         assert np.array_equal(done[k], full[k]), k
 
 
-@pytest.mark.parametrize("n", [65, 100, 128])
+@pytest.mark.parametrize("n", [40, 64, 65, 100, 128])
 @pytest.mark.parametrize("dens", DENSITIES)
 def test_int8_fused_vs_oracle_and_f64(pa, po, rng, n, dens):
     """The fused pass on the int8 stage (G, Σψ′, Σℓ, Σy²) against the oracle (1e-12) and
@@ -213,7 +214,7 @@ def test_int8_gram_stays_fp64(pa, rng):
     assert rel_err(g, xc @ xc.T) <= TOL
 
 
-@pytest.mark.parametrize("n", [72, 128])
+@pytest.mark.parametrize("n", [40, 64, 72, 128])
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("tanh", 0.5), ("exp", 1.0), ("exp", 0.3)])
 def test_screen_bound_holds(pa, rng, n, dens):
     """The line-search screen's bound covers the exact pass: |Σℓ_exact − Σℓ_screen| ≤ bound
@@ -244,8 +245,13 @@ def test_screen_unavailable_shapes(pa, rng):
     x = laplace_mix(rng, 40, 3000)
     ctx = pa.DeviceContext(0)
     ctx.load(x)
-    with pytest.raises(pa.ComputationError):  # nc ≤ 64: no int8 stage
-        ctx.eval_loss_screen(np.eye(40), x.mean(axis=1), pa.DensityType.tanh())
+    with pytest.raises(pa.ComputationError):  # nc ≤ 32: no int8 stage
+        ctx.eval_loss_screen(np.eye(40)[:20], x.mean(axis=1), pa.DensityType.tanh())
+    x = laplace_mix(rng, 80, 3000)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    with pytest.raises(pa.ComputationError):  # 32 < nc ≤ 64 needs nf ≤ 64
+        ctx.eval_loss_screen(np.eye(80)[:50], x.mean(axis=1), pa.DensityType.tanh())
     x = laplace_mix(rng, 100, 3000)
     ctx = pa.DeviceContext(0)
     ctx.load(x)
@@ -256,7 +262,7 @@ def test_screen_unavailable_shapes(pa, rng):
         ctx.eval_loss_screen(np.eye(100), x.mean(axis=1), pa.DensityType.tanh())
 
 
-@pytest.mark.parametrize("n,seed", [(128, 42), (96, 7)])
+@pytest.mark.parametrize("n,seed", [(128, 42), (96, 7), (64, 42), (48, 3)])
 def test_screened_fit_bit_identical(pa, n, seed, capfd, monkeypatch):
     """A Picard-O fit with the line-search screen (default) and without it (int8-exact):
     identical iterations and bit-identical unmixing — the screen rejects only tries the

@@ -11,12 +11,18 @@ if d.get("whole_fit"):
                                                                      w["passes_per_iter"]))
 for r in d.get("roofline_kernels", []):
     print("  %-44s %8.2f ms  %.3f of peak %.1f (%.3f of fp64 MFMA)  traffic %s" % (
-        r["kernel"], r["avg_kernel_ms"], r["frac"], r["peak"], r.get("frac_of_fp64_mfma_peak", r["frac"]), r["traffic"]))
+        r["kernel"], r["avg_kernel_ms"], r.get("frac_of_executed_mix_peak", r["frac"]), r.get("executed_mix_peak_tflops", r["peak"]),
+        r.get("frac_of_fp64_mfma_peak", r["frac"]), r["traffic"]))
 for k, c in (d.get("other_configs") or {}).items():
     print("  %s %-48s iters %4d  setup %.2fs  iter %.2fs  %.3g samples/s/iter  passes %d  amari %.2e" % (
         k, c["workload"], c["iters_to_tol"], c["setup_s"], c["iterations_s"], c["samples_per_s_per_iter"],
         c["passes"], c["amari_vs_true_mixing"]))
     print("      kernel ms", c["kernel_ms"], "launches", c["kernel_launches"])
+    for key in ("cpu_baseline", "cpu_baseline_jade"):
+        if c.get(key):
+            print("      %s %.4g %s (%s cores)" % (key, c[key]["value"], c[key]["unit"], c[key]["cores"]))
+if d.get("cpu_baseline"):
+    print("  C3 cpu_baseline %.4g %s (%s cores)" % (d["cpu_baseline"]["value"], d["cpu_baseline"]["unit"], d["cpu_baseline"]["cores"]))
 if d.get("transform"):
     t = d["transform"]
     print("  transform %s %.2f ms  %.1f TF/s (%.3f of MFMA peak)  %.0f GB/s  bound %.2f ms" % (
