@@ -1119,8 +1119,20 @@ __device__ __forceinline__ double reduce_partials(const double* __restrict__ p, 
                                                   double (*red)[RED_OUT]) {
   const int g = threadIdx.x / RED_OUT, o = threadIdx.x % RED_OUT;
   double s = 0.0;
-  if (ok)
-    for (int w = nwg * g / 4; w < nwg * (g + 1) / 4; ++w) s += p[(size_t)w * pstride];
+  if (ok) {
+    // loads 8 at a time (in flight together), added in the same order: the latency of a
+    // serial chain of 128 L2/HBM loads was most of this kernel's time at small T
+    const int w1 = nwg * (g + 1) / 4;
+    int w = nwg * g / 4;
+    for (; w + 8 <= w1; w += 8) {
+      double v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = p[(size_t)(w + j) * pstride];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; w < w1; ++w) s += p[(size_t)w * pstride];
+  }
   red[g][o] = s;
   __syncthreads();
   return (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
@@ -2485,13 +2497,18 @@ struct DeviceCtx : Evaluator {
     // NB = 4 without H, nf ≤ 64: k_eval_fused<4> on the int8-digit Y stage
     constexpr bool OZ4 = NB == 4 && !H && D != DENS_LINEAR;
     const bool oz4 = OZ4 && oz_ok && oz_kso() == 1;
+    // … and its warp-specialised form on the centred resident X (PICARD_NO_WS4=1: the 8-wave kernel)
+    const bool ws4 = NB == 4 && !H && dmu == nullptr && nf <= 64 && !no_ws4_;
     auto kws = oz ? k_eval_fused_ws<D, Q, true> : k_eval_fused_ws<D, Q, false>;
     auto kfu = oz4 ? k_eval_fused<NB, H, D, Q, OZ4> : k_eval_fused<NB, H, D, Q, false>;
-    lds_attr(ws ? (const void*)kws : (const void*)kfu, 160 * 1024 - EXP_TAB_BYTES);
+    auto kw4 = oz4 ? k_eval_fused_ws4<D, Q, OZ4> : k_eval_fused_ws4<D, Q, false>;
+    lds_attr(ws ? (const void*)kws : ws4 ? (const void*)kw4 : (const void*)kfu, 160 * 1024 - EXP_TAB_BYTES);
     HIP_OK(hipEventRecord(ev[1], stream));
     if (ws)
       kws<<<nwg, WS_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part, d_xsl, d_xsc,
                                            d_wsl, d_wsc);
+    else if (ws4)
+      kw4<<<nwg, WS_THREADS, lds, stream>>>(X, ldx, (int)nf, d_w, alpha, bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc);
     else
       kfu<<<nwg, FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, d_w, dmu, alpha, bpw, n_blocks, part, d_xsl,
                                                d_xsc, d_wsl, d_wsc);
@@ -2965,6 +2982,7 @@ struct DeviceCtx : Evaluator {
     if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
   }
   uint64_t n_screen_passes_ = 0;
+  bool no_ws4_ = std::getenv("PICARD_NO_WS4") != nullptr;
   // the tanh screen evaluates ℓ in fp32 (PICARD_SCREEN_F64=1: the fp64 row terms of the
   // exact pass, a tighter bound at a higher cost)
   bool screen_f32_ = std::getenv("PICARD_SCREEN_F64") == nullptr;

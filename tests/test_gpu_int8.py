@@ -370,3 +370,30 @@ def test_int8_sources(pa, rng, nc, nf, t):
     # sample's scale 2^e_t, not the whole matrix's)
     col = np.abs(got - f64).max(axis=0) / np.maximum(np.abs(f64).max(axis=0), 1e-300)
     assert col.max() <= 1e-13, col.max()
+
+
+@pytest.mark.parametrize("n,t", [(40, 5003), (64, 100_003), (33, 777)])
+@pytest.mark.parametrize("stage", ["auto", "f64"])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
+def test_ws4_bit_identical_to_8wave(pa, rng, n, t, stage, dens, monkeypatch):
+    """The warp-specialised NB = 4 fused pass (k_eval_fused_ws4) against the 8-wave
+    k_eval_fused<4> (PICARD_NO_WS4=1), on either Y stage: every statistic bit for bit
+    (same partition, G-tile map and k order, lane map, row-term order)."""
+    x = laplace_mix(rng, n, t)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    out = []
+    for no_ws4 in (False, True):
+        if no_ws4:
+            monkeypatch.setenv("PICARD_NO_WS4", "1")
+        ctx = pa.DeviceContext(0)
+        ctx.load(x)
+        ctx.set_y_stage(stage)
+        out.append((ctx.eval(w, mu, d, False), ctx.int8_passes, ctx.gram(mu)))
+        ctx.close()
+    (a, na, ga), (b, nb_, gb) = out
+    assert na == nb_ and (na == 1) == (stage == "auto" and n > 32)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(ga, gb)  # the whitening Gram takes the same kernels (fp64)
