@@ -1317,6 +1317,110 @@ k_tiled_yw(const double* __restrict__ X, uint64_t ldx, uint64_t n_in, int nf, in
   }
 }
 
+// Phase 1 on the int8 digit stage (KSO k-steps of 64 features: nf ≤ 128 → 2, ≤ 256 → 4):
+// the same roles, fragment layout, density, row terms and store/barrier schedule as
+// k_tiled_yw (MODE 0 / 1, one feature chunk), with wave ib's Y tile formed by
+// oz_ystage + oz_combine (ozaki.inc) from the digit image of X and the W digits held in
+// VGPRs (7·KSO v4i per lane) — W read once per launch as k_tiled_yw's fragments are. Per
+// 16-sample block the 7·KSO planes (1 KiB each) and 16 scales are staged by LDS-DMA,
+// item w + 8u of wave w. Y has the accuracy of the fp64 stage (ozaki.inc); the full
+// (MODE 0) and loss-only (MODE 1) passes run the same arithmetic, so their Σℓ, Σy² agree.
+template <int KSO, int DENS, int MODE>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_tiled_yw_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc, const uint8_t* __restrict__ wsl_g,
+              const double* __restrict__ wsc, int ncp, double alpha, uint64_t bpw, uint64_t n_blocks,
+              double* __restrict__ partials, int accumulate, double* ybuf, double* __restrict__ pbuf,
+              double* __restrict__ dbuf, uint64_t nwgx) {
+  static_assert(MODE == 0 || MODE == 1, "one feature chunk");
+  constexpr int TILE = oz_block_bytes<KSO>(), NITEM = OZ_SLICES * KSO + 1, NU = (NITEM + 7) / 8;
+  constexpr int SLOT = TILE + 256;  // bytes per staged block: digit planes, 16 scales
+  constexpr int KSW = KSO < 2 ? 2 : KSO;  // k-step stride of the W digit image (DeviceCtx::wsl_ksw)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  uint64_t wx;
+  int role;
+  if (!xcd_decode((nib + 7) / 8, nwgx, wx, role)) return;
+  const int ib = role * 8 + wave;
+  const bool active = ib < nib;
+  const int row = ib * 16 + lr;
+  const double alpha_ = alpha, inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
+  extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
+  uint8_t* xs0 = (uint8_t*)smem;  // [2][SLOT]
+  v4i wsl[OZ_SLICES][KSO];
+#pragma unroll
+  for (int a = 0; a < OZ_SLICES; ++a)
+#pragma unroll
+    for (int k = 0; k < KSO; ++k)
+      wsl[a][k] = active ? *(const v4i*)(wsl_g + (size_t)(((ib * OZ_SLICES + a) * KSW + k) * 64 + lane) * 16)
+                         : v4i{0, 0, 0, 0};
+  const double rsc = active ? wsc[row] : 0.0;
+  RowAcc racc;
+  const uint64_t b_begin = wx * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  auto stage = [&](uint64_t b, uint8_t* xs) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int it = wave + 8 * u;
+      if (it < NITEM - 1)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(xsl + b * TILE + it * 1024 + lane * 16),
+                                         (lds_vptr)(xs + it * 1024), 16, 0, 0);
+      else if (it == NITEM - 1)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)((const uint32_t*)(xsc + b * 16) + (lane & 31)),
+                                         (lds_vptr)(xs + TILE), 4, 0, 0);
+    }
+  };
+  if (b_begin < b_end) {
+    stage(b_begin, xs0);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      const size_t f0 = tl_frag(b >> 2, ib, (int)(b & 3), 0, nib) + lane;
+      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * SLOT);
+      __builtin_amdgcn_sched_barrier(0);  // the DMA stays ahead of this block's stores (dma_barrier)
+      if (active) {
+        const uint8_t* tile = xs0 + cur * SLOT;
+        v4i acc[OZ_SLICES];
+        oz_ystage<OZ_SLICES - 1, KSO>(tile, lane, wsl, acc);
+        const double* scd = (const double*)(tile + TILE);
+        const double x4[4] = {scd[lk], scd[lk + 4], scd[lk + 8], scd[lk + 12]};
+        const d4 yv = oz_combine(acc, rsc, x4);
+        if constexpr (MODE == 0) {
+          double psi[4], dpsi[4];
+          density_acc4<DENS, true, true, 1>(yv, alpha_, m2a, s_exp_tab, racc, psi, dpsi);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ybuf[f0 + 64 * r] = yv[r];
+            pbuf[f0 + 64 * r] = psi[r];
+            if (dbuf) dbuf[f0 + 64 * r] = dpsi[r];
+          }
+        } else {
+          loss_acc4<DENS, true, 1>(yv, alpha_, m2a, s_exp_tab, racc);
+        }
+        if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc);
+      }
+      // this wave's LDS-DMA of block b + 1 landed; its y / ψ (/ ψ′) stores may still be in flight
+      if (!active || MODE == 1) dma_barrier<0>();
+      else if (dbuf) dma_barrier<12>();
+      else dma_barrier<8>();
+      cur ^= 1;
+    }
+  }
+  const int nfac = b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0;  // one density call per block
+  double rs_d = acc_dpsi<DENS>(racc), rs_l = acc_ll<DENS>(racc, inv_alpha, nfac), rs_q = racc.q;
+  rs_d += __shfl_xor(rs_d, 16); rs_d += __shfl_xor(rs_d, 32);
+  rs_l += __shfl_xor(rs_l, 16); rs_l += __shfl_xor(rs_l, 32);
+  rs_q += __shfl_xor(rs_q, 16); rs_q += __shfl_xor(rs_q, 32);
+  if (active && lk == 0) {
+    double* out = partials + (size_t)wx * 3 * ncp;
+    const double v[3] = {MODE == 0 ? rs_d : 0.0, rs_l, rs_q};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[c * ncp + row] = accumulate ? out[c * ncp + row] + v[c] : v[c];
+  }
+}
+
 // Phase 2 staged through LDS: blockIdx.x = 128×128 output tile (ti, tj),
 // blockIdx.y = T split. Per 16-sample sub-block the workgroup copies the ψ
 // (and ψ′) fragments of its 8 row blocks ti and the y fragments of row blocks
@@ -2750,16 +2854,39 @@ struct DeviceCtx : Evaluator {
   }
   // one T chunk: phase 1 over the feature chunks (partial y through the y
   // buffer), then phase 2 (mode 0)
+  // phase 1 on the int8 digit stage: one launch over the T chunk starting at tile t0
+  template <int KSO, int D>
+  void yw_oz_launch(int mode, int ncp, double alpha, uint64_t ntl, int nwg1, bool acc, uint64_t t0, double* yb,
+                    double* pb, double* db) {
+    const uint64_t n_blocks = ntl * 4;
+    const uint64_t bpw = (n_blocks + nwg1 - 1) / nwg1;
+    const int nroles = (ncp / 16 + 7) / 8;
+    const size_t lds = (size_t)2 * (oz_block_bytes<KSO>() + 256);
+    auto k = mode == 0 ? k_tiled_yw_oz<KSO, D, 0> : k_tiled_yw_oz<KSO, D, 1>;
+    lds_attr((const void*)k, (int)lds);
+    k<<<xcd_grid(nwg1, nroles), FUSED_THREADS, lds, stream>>>(d_xsl + t0 * 4 * oz_block_bytes<KSO>(), d_xsc + t0 * TL_TT,
+                                                              d_wsl, d_wsc, ncp, alpha, bpw, n_blocks, d_trow,
+                                                              acc ? 1 : 0, yb, pb, db, (uint64_t)nwg1);
+  }
   template <int D>
   void tiled_launch(int mode, int ks, int ncp, double alpha, uint64_t ntl, bool need_h, int nsplit, int nwg1, bool acc,
-                    const double* X0) {
+                    const double* X0, bool oz, uint64_t t0) {
     const size_t chunk = (size_t)ncp * ntl * TL_TT;
     constexpr bool dfromp = D == DENS_TANH;  // ψ′ = α(1 − ψ²) formed in phase 2
     double* yb = d_tbuf;
     double* pb = d_tbuf + chunk;
     double* db = need_h && !dfromp ? d_tbuf + 2 * chunk : nullptr;
     const uint64_t kc = 4 * (uint64_t)ks;  // features per chunk
-    for (uint64_t k0 = 0; k0 < nf; k0 += kc) {
+    if constexpr (D != DENS_LINEAR) {
+      if (oz) {  // all features in one launch (nf ≤ 256)
+        if (oz_kso() == 4) yw_oz_launch<4, D>(mode, ncp, alpha, ntl, nwg1, acc, t0, yb, pb, db);
+        else if (oz_kso() == 2) yw_oz_launch<2, D>(mode, ncp, alpha, ntl, nwg1, acc, t0, yb, pb, db);
+        else yw_oz_launch<1, D>(mode, ncp, alpha, ntl, nwg1, acc, t0, yb, pb, db);
+        HIP_OK(hipGetLastError());
+        ++n_int8_passes_;
+      }
+    }
+    for (uint64_t k0 = 0; k0 < nf && !oz; k0 += kc) {
       const bool last = k0 + kc >= nf;
       yw_launch<D>(ks, last ? mode : 2, ncp, alpha, ntl, nwg1, acc, X0 + k0 * ldx, std::min<uint64_t>(kc, nf - k0),
                    d_w + k0 * ncp, yb, pb, db, k0 > 0 ? yb : nullptr);
@@ -2811,17 +2938,22 @@ struct DeviceCtx : Evaluator {
     if (mode == 0) ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
     ensure(d_trow, cap_trow, (size_t)nwg1 * 3 * ncp);
     const int td = tiled_dens(dens, alpha);
+    // phase 1 on the int8 digit stage (nf ≤ 256; not the whitening Gram), after every buffer
+    // of the pass is allocated (an allocation may release an unpinned image)
+    bool oz = y_stage_ != 1 && nf <= 256 && td != DENS_LINEAR && ensure_xsl();
+    if (oz) upload_wsl(w, nc);
+    oz = oz && xsl_valid_;
     for (uint64_t t0 = 0; t0 < std::max<uint64_t>(n_tiles, 1); t0 += ct) {
       const uint64_t ntl = std::min<uint64_t>(ct, std::max<uint64_t>(n_tiles, 1) - t0);
       const bool acc = t0 > 0;
       const double* X0 = X + t0 * TL_TT;
       switch (td) {
-        case DENS_TANH: tiled_launch<DENS_TANH>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
-        case DENS_EXP: tiled_launch<DENS_EXP>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
-        case DENS_CUBE: tiled_launch<DENS_CUBE>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
-        case DENS_TANH_S: tiled_launch<DENS_TANH_S>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
-        case DENS_EXP_S: tiled_launch<DENS_EXP_S>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
-        default: tiled_launch<DENS_LINEAR>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0); break;
+        case DENS_TANH: tiled_launch<DENS_TANH>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, oz, t0); break;
+        case DENS_EXP: tiled_launch<DENS_EXP>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, oz, t0); break;
+        case DENS_CUBE: tiled_launch<DENS_CUBE>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, oz, t0); break;
+        case DENS_TANH_S: tiled_launch<DENS_TANH_S>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, oz, t0); break;
+        case DENS_EXP_S: tiled_launch<DENS_EXP_S>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, oz, t0); break;
+        default: tiled_launch<DENS_LINEAR>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, false, t0); break;
       }
     }
     const size_t total = (size_t)(mode == 0 ? (need_h ? 2 : 1) * nc * nc : 0) + 3 * nc;
@@ -2883,11 +3015,13 @@ struct DeviceCtx : Evaluator {
   // … and the NB = 4 forms: 32 < nc ≤ 64 with nf ≤ 64 (a 1-k-step image)
   bool oz4_shape(size_t nc) const { return y_stage_ != 1 && pick_nb(nc) == 4 && nf <= 64 && nf > 0; }
   bool oz_any(size_t nc) const { return oz_shape(nc) || oz4_shape(nc); }
-  int oz_kso() const { return nf <= 64 ? 1 : 2; }  // k-steps of the resident X's digit image
-  size_t oz_bb() const { return oz_kso() == 1 ? (size_t)oz_block_bytes<1>() : (size_t)oz_block_bytes<2>(); }
+  // k-steps of 64 features of the resident X's digit image (nf ≤ 256)
+  int oz_kso() const { return nf <= 64 ? 1 : nf <= 128 ? 2 : 4; }
+  size_t oz_bb() const { return (size_t)oz_kso() * OZ_SLICES * 1024; }
+  int wsl_ksw() const { return oz_kso() == 4 ? 4 : 2; }  // k-step stride of the W digit image
   bool ensure_xsl() {
     if (xsl_valid_) return true;
-    if (xsl_failed_) return false;
+    if (xsl_failed_ || nf > 256) return false;
     // the scratch of the Σ 2^e_t sum first: an allocation here may release the image
     const int nwg_e = (int)std::max<uint64_t>(1, std::min<uint64_t>((ldx + 4095) / 4096, 1024));
     ensure(d_shift_part, cap_shift_part, (size_t)nwg_e + 1);
@@ -2912,7 +3046,8 @@ struct DeviceCtx : Evaluator {
     }
     const unsigned grid = (unsigned)std::min<uint64_t>(n_blocks, (uint64_t)n_cu * 16);
     if (oz_kso() == 1) k_slice_x<1><<<grid, 64, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
-    else k_slice_x<2><<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
+    else if (oz_kso() == 2) k_slice_x<2><<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
+    else k_slice_x<4><<<grid, 256, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     HIP_OK(hipGetLastError());
     {  // Σ_t 2^e_t of this shard (padding included: it only loosens the screen's bound)
       const int nwg = nwg_e;
@@ -2938,20 +3073,25 @@ struct DeviceCtx : Evaluator {
   void upload_wsl(const double* w, size_t nc) {
     if (wsl_nc_ == nc && wsl_w_.size() == nc * nf && std::memcmp(wsl_w_.data(), w, nc * nf * sizeof(double)) == 0)
       return;
-    constexpr size_t IMG = (size_t)8 * OZ_SLICES * 2 * 64 * 16;
+    // up to 16 row blocks (256 rows); k-step stride wsl_ksw() (2: the NB = 8 / 4 kernels,
+    // 4: the tiled pass at nf ≤ 256)
+    constexpr size_t IMG_MAX = (size_t)16 * OZ_SLICES * 4 * 64 * 16;
+    const int ksw = wsl_ksw();
+    const size_t img_bytes = (size_t)((nc + 15) / 16) * OZ_SLICES * ksw * 64 * 16;
     if (!d_wsl) {
-      HIP_OK(hipMalloc(&d_wsl, IMG));
-      HIP_OK(hipMalloc(&d_wsc, 128 * sizeof(double)));
+      HIP_OK(hipMalloc(&d_wsl, IMG_MAX));
+      HIP_OK(hipMalloc(&d_wsc, 256 * sizeof(double)));
     }
-    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, IMG + 128 * sizeof(double));
-    double* sc = (double*)(img + IMG);
-    std::memset(img, 0, IMG);
-    for (int i = 0; i < 128; ++i) sc[i] = 0x1p-12;
-    oz_split_rows(w, nc, nf, img, sc);  // host_linalg.cpp: rows split over the host threads
+    if (nc > 256) throw computation_error("int8 W image: nc > 256");
+    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, IMG_MAX + 256 * sizeof(double));
+    double* sc = (double*)(img + IMG_MAX);
+    std::memset(img, 0, img_bytes);
+    for (int i = 0; i < 256; ++i) sc[i] = 0x1p-12;
+    oz_split_rows(w, nc, nf, img, sc, ksw);  // host_linalg.cpp: rows split over the host threads
     wsl_w_.assign(w, w + nc * nf);
     wsl_nc_ = nc;
-    HIP_OK(hipMemcpyAsync(d_wsl, img, IMG, hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(d_wsc, sc, 128 * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsl, img, img_bytes, hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsc, sc, 256 * sizeof(double), hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
   // NB = 8 (64 < nc ≤ 128) or NB = 4 (32 < nc ≤ 64, nf ≤ 64; partition in 32-sample blocks,

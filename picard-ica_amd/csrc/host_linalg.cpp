@@ -532,7 +532,7 @@ bool invert_matrix(const Mat& m, Mat* out) {
 // of 64·w·2^-f_i by a shifter rint (exact for |v| < 2^51), ±128/±129 folded into the digit
 // above; img[wave][digit][kstep][lane][16 B] as the i8 MFMA B operand. A NaN / ±inf weight
 // makes the row's scale NaN (zero digits), as the fp64 stage would give NaN.
-void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc) {
+void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc, int ksw) {
   constexpr double SH = 0x1.8p52;
   constexpr int OZ_SLICES = 7;
   // rows are independent (each writes its own digit bytes and scale): split over the threads
@@ -570,7 +570,7 @@ void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* 
       }
       const size_t s = k >> 6, lane = n + 16 * ((k >> 4) & 3), j = k & 15;
       for (int a = 0; a < OZ_SLICES; ++a)
-        img[(((wave * OZ_SLICES + a) * 2 + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
+        img[(((wave * OZ_SLICES + a) * ksw + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
     }
   }
 }

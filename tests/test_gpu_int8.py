@@ -397,3 +397,35 @@ def test_ws4_bit_identical_to_8wave(pa, rng, n, t, stage, dens, monkeypatch):
     for k in a:
         assert np.array_equal(a[k], b[k]), k
     assert np.array_equal(ga, gb)  # the whitening Gram takes the same kernels (fp64)
+
+
+@pytest.mark.parametrize("nc,nf,h", [(256, 256, True), (256, 256, False), (200, 256, True), (150, 180, True),
+                                     (100, 128, True), (40, 40, True)])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
+def test_tiled_int8_vs_oracle_and_f64(pa, po, rng, nc, nf, h, dens):
+    """The tiled two-phase pass (nc > 128, or H at nc > 64 — BASELINE C4's path) with phase 1
+    on the int8 digit stage (k_tiled_yw_oz, nf ≤ 256): every statistic against the oracle
+    (1e-12) and the fp64 stage (1e-13); its loss-only form (phase 1 alone) gives the full
+    pass's Σℓ and Σy² bit for bit."""
+    x = laplace_mix(rng, nf, 9001)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    w = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    got = ctx.eval(w, mu, d, h)
+    tiled = nc > 128 or (h and nc > 64)
+    assert (ctx.int8_passes >= 1) == tiled or not tiled
+    want = po.pass_stats(w, mu, x, density_of(po, d), h)
+    for k in want:
+        assert rel_err(got[k], want[k]) <= TOL, (k, rel_err(got[k], want[k]))
+    lo, _, done = ctx.eval_split(w, mu, d, h)
+    assert np.array_equal(lo["ll"], got["ll"]) and np.array_equal(lo["y2"], got["y2"])
+    for k in got:
+        assert np.array_equal(done[k], got[k]), k
+    ctx.set_y_stage("f64")
+    n8 = ctx.int8_passes
+    ref = ctx.eval(w, mu, d, h)
+    assert ctx.int8_passes == n8
+    for k in want:
+        assert rel_err(got[k], ref[k]) <= TOL_MODES, (k, rel_err(got[k], ref[k]))
