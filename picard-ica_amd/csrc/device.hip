@@ -1790,6 +1790,120 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
   }
 }
 
+// k_multi_loss2 on the int8 digit stage (nf ≤ 256, KSO k-steps): wave w forms the full-K Yᵀ
+// (w < 4) or Zᵀ (w ≥ 4) tile of row block 4·role + (w & 3) from the digit image of X and the
+// W / Z digits held in VGPRs (image row blocks 0–15: W, 16–31: Z = D·W), the two tiles meet in
+// LDS, and the pair evaluates the tries on y = Y + α_j·Z exactly as k_multi_loss2 does (wave
+// w takes the tries j ≡ w >> 2 mod 2). Y and Z carry fp64-GEMM accuracy (ozaki.inc); like the
+// fp64 form, Y_α = Y + α·Z agrees with a per-try pass to rounding.
+template <int KSO, int DENS, bool NEED_Q>
+__global__ void __launch_bounds__(FUSED_THREADS, 2)
+k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc, const uint8_t* __restrict__ wsl_g,
+                 const double* __restrict__ wsc, int ncp, double alpha, const double* __restrict__ alphas, int na,
+                 uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials, uint64_t nwgx) {
+  constexpr int TILE = oz_block_bytes<KSO>(), NITEM = OZ_SLICES * KSO + 1, NU = (NITEM + 7) / 8;
+  constexpr int SLOT = TILE + 256, KSW = KSO < 2 ? 2 : KSO;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  const int rb = wave & 3, yz = wave >> 2;
+  uint64_t wx;
+  int role;
+  if (!xcd_decode((nib + 3) / 4, nwgx, wx, role)) return;
+  const int ib = role * 4 + rb;
+  const bool active = ib < nib;
+  const int row = ib * 16 + lr;
+  const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
+  extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
+  uint8_t* xs0 = (uint8_t*)smem;                          // [2][SLOT]
+  double* ex0 = (double*)(xs0 + 2 * SLOT);                // [2][4 row blocks][Y, Z][4][64]
+  v4i wsl[OZ_SLICES][KSO];
+  const int wb = yz * 16 + ib;  // image row block: W (yz = 0) or Z (1)
+#pragma unroll
+  for (int a = 0; a < OZ_SLICES; ++a)
+#pragma unroll
+    for (int k = 0; k < KSO; ++k)
+      wsl[a][k] = active ? *(const v4i*)(wsl_g + (size_t)(((wb * OZ_SLICES + a) * KSW + k) * 64 + lane) * 16)
+                         : v4i{0, 0, 0, 0};
+  const double rsc = active ? wsc[yz * 256 + row] : 0.0;
+  double aj[ML2_TRIES];
+  RowAcc racc[ML2_TRIES];
+#pragma unroll
+  for (int u = 0; u < ML2_TRIES; ++u) aj[u] = (yz + 2 * u < na) ? alphas[yz + 2 * u] : 0.0;
+  const int my_na = na > yz ? (na - yz + 1) / 2 : 0;
+  const uint64_t b_begin = wx * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  auto stage = [&](uint64_t b, uint8_t* xs) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int it = wave + 8 * u;
+      if (it < NITEM - 1)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(xsl + b * TILE + it * 1024 + lane * 16),
+                                         (lds_vptr)(xs + it * 1024), 16, 0, 0);
+      else if (it == NITEM - 1)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)((const uint32_t*)(xsc + b * 16) + (lane & 31)),
+                                         (lds_vptr)(xs + TILE), 4, 0, 0);
+    }
+  };
+  auto exch = [&](int buf, int w_yz, int r) -> double* {
+    return ex0 + (((buf * 4 + rb) * 2 + w_yz) * 4 + r) * 64 + lane;
+  };
+  if (b_begin < b_end) {
+    stage(b_begin, xs0);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * SLOT);
+      if (active) {
+        const uint8_t* tile = xs0 + cur * SLOT;
+        v4i acc[OZ_SLICES];
+        oz_ystage<OZ_SLICES - 1, KSO>(tile, lane, wsl, acc);
+        const double* scd = (const double*)(tile + TILE);
+        const double x4[4] = {scd[lk], scd[lk + 4], scd[lk + 8], scd[lk + 12]};
+        const d4 v = oz_combine(acc, rsc, x4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *exch(cur, yz, r) = v[r];
+      }
+      __syncthreads();  // exchange visible; this wave's LDS-DMA of block b + 1 landed
+      if (active) {
+        d4 yv, zv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          yv[r] = *exch(cur, 0, r);
+          zv[r] = *exch(cur, 1, r);
+        }
+#pragma unroll
+        for (int u = 0; u < ML2_TRIES; ++u) {
+          if (u < my_na) {
+            d4 yj;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj[u], zv[r], yv[r]);
+            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, s_exp_tab, racc[u]);
+            if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
+          }
+        }
+      }
+      cur ^= 1;
+    }
+  }
+  double* out = partials + (size_t)wx * ML_NA * 2 * ncp;
+#pragma unroll
+  for (int u = 0; u < ML2_TRIES; ++u) {
+    if (u < my_na) {
+      double l = acc_ll<DENS>(racc[u], inv_alpha, b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0), q = racc[u].q;
+      l += __shfl_xor(l, 16); l += __shfl_xor(l, 32);
+      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+      if (active && lk == 0) {
+        const int j = yz + 2 * u;
+        out[(j * 2 + 0) * ncp + row] = l;
+        out[(j * 2 + 1) * ncp + row] = q;
+      }
+    }
+  }
+}
+
 // stats[e] for the tiled path: G/H from slabs (sum over splits), rows from phase-1 partials.
 // Row terms from k_tiled_yw are raw (finalize_row with dens ≥ 0); k_tiled_y's are final (dens < 0).
 __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, const double* __restrict__ rows,
@@ -2712,6 +2826,25 @@ struct DeviceCtx : Evaluator {
     k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(X, ldx, n_local_, (int)nf, ncp, dw, dz, dmu, alpha, dal, na,
                                                              bpw, n_blocks, part, (uint64_t)nwg);
   }
+  template <int KSO, int D>
+  void multi2_oz_launch(int ncp, double alpha, const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks,
+                        double* part) {
+    const int nroles = (ncp / 16 + 3) / 4;
+    const size_t lds = (size_t)2 * (oz_block_bytes<KSO>() + 256) + (size_t)2 * 4 * 2 * 4 * 64 * sizeof(double);
+    auto k = want_y2 ? k_multi_loss2_oz<KSO, D, true> : k_multi_loss2_oz<KSO, D, false>;
+    lds_attr((const void*)k, (int)lds);
+    k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, ncp, alpha, dal, na, bpw,
+                                                             n_blocks, part, (uint64_t)nwg);
+  }
+  template <int D>
+  void multi2_oz_dispatch(int ncp, double alpha, const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks,
+                          double* part) {
+    switch (oz_kso()) {
+      case 1: multi2_oz_launch<1, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      case 2: multi2_oz_launch<2, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      default: multi2_oz_launch<4, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+    }
+  }
   template <int D>
   void multi2_dispatch(int ks, int ncp, const double* dw, const double* dz, const double* dmu, double alpha,
                        const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks, double* part) {
@@ -2747,7 +2880,21 @@ struct DeviceCtx : Evaluator {
       const int nwg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)2 * n_cu / nroles, n_blocks));
       const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
       double* part = ensure(d_part, cap_part, (size_t)nwg * pst);
+      double* st0 = ensure(d_stats, cap_stats, (size_t)2 * na * nc);
+      (void)st0;
+      // Y and Z on the int8 digit stage (after the pass buffers: an allocation may release the image)
+      bool oz = y_stage_ != 1 && dmu == nullptr && ensure_xsl();
+      if (oz) upload_wsl2(w, z, nc);
+      oz = oz && xsl_valid_;
       HIP_OK(hipEventRecord(ev[1], stream));
+      if (oz) {
+        switch (d.kind) {
+          case DENS_TANH: multi2_oz_dispatch<DENS_TANH>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+          case DENS_EXP: multi2_oz_dispatch<DENS_EXP>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+          default: multi2_oz_dispatch<DENS_CUBE>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+        }
+        ++n_int8_passes_;
+      } else
       switch (d.kind) {
         case DENS_TANH: multi2_dispatch<DENS_TANH>(ks, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
         case DENS_EXP: multi2_dispatch<DENS_EXP>(ks, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
@@ -3070,20 +3217,41 @@ struct DeviceCtx : Evaluator {
   // (exact round-half-even for |v| < 2^51, no libm call on the host).
   std::vector<double> wsl_w_;
   size_t wsl_nc_ = 0;
+  static constexpr size_t WSL_IMG_MAX = (size_t)32 * OZ_SLICES * 4 * 64 * 16;  // 32 row blocks × 4 k-steps
+  void alloc_wsl() {
+    if (!d_wsl) {
+      HIP_OK(hipMalloc(&d_wsl, WSL_IMG_MAX));
+      HIP_OK(hipMalloc(&d_wsc, 512 * sizeof(double)));
+    }
+  }
+  // the multi-try pass: W in row blocks 0–15 (scales 0–255), Z = D·W in 16–31 (256–511)
+  void upload_wsl2(const double* w, const double* z, size_t nc) {
+    alloc_wsl();
+    if (nc > 256) throw computation_error("int8 W image: nc > 256");
+    const int ksw = wsl_ksw();
+    const size_t half = (size_t)16 * OZ_SLICES * ksw * 64 * 16;
+    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, WSL_IMG_MAX + 512 * sizeof(double));
+    double* sc = (double*)(img + WSL_IMG_MAX);
+    std::memset(img, 0, 2 * half);
+    for (int i = 0; i < 512; ++i) sc[i] = 0x1p-12;
+    oz_split_rows(w, nc, nf, img, sc, ksw);
+    oz_split_rows(z, nc, nf, img + half, sc + 256, ksw);
+    wsl_nc_ = 0;  // the image no longer holds a single W
+    HIP_OK(hipMemcpyAsync(d_wsl, img, 2 * half, hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsc, sc, 512 * sizeof(double), hipMemcpyHostToDevice, stream));
+    pin_release(pin_wsl_);
+  }
   void upload_wsl(const double* w, size_t nc) {
     if (wsl_nc_ == nc && wsl_w_.size() == nc * nf && std::memcmp(wsl_w_.data(), w, nc * nf * sizeof(double)) == 0)
       return;
     // up to 16 row blocks (256 rows); k-step stride wsl_ksw() (2: the NB = 8 / 4 kernels,
-    // 4: the tiled pass at nf ≤ 256)
-    constexpr size_t IMG_MAX = (size_t)16 * OZ_SLICES * 4 * 64 * 16;
+    // 4: the tiled pass at nf ≤ 256); the multi-try pass puts Z in row blocks 16–31
+    constexpr size_t IMG_MAX = WSL_IMG_MAX;
     const int ksw = wsl_ksw();
     const size_t img_bytes = (size_t)((nc + 15) / 16) * OZ_SLICES * ksw * 64 * 16;
-    if (!d_wsl) {
-      HIP_OK(hipMalloc(&d_wsl, IMG_MAX));
-      HIP_OK(hipMalloc(&d_wsc, 256 * sizeof(double)));
-    }
+    alloc_wsl();
     if (nc > 256) throw computation_error("int8 W image: nc > 256");
-    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, IMG_MAX + 256 * sizeof(double));
+    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, IMG_MAX + 512 * sizeof(double));
     double* sc = (double*)(img + IMG_MAX);
     std::memset(img, 0, img_bytes);
     for (int i = 0; i < 256; ++i) sc[i] = 0x1p-12;

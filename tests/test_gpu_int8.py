@@ -429,3 +429,29 @@ def test_tiled_int8_vs_oracle_and_f64(pa, po, rng, nc, nf, h, dens):
     assert ctx.int8_passes == n8
     for k in want:
         assert rel_err(got[k], ref[k]) <= TOL_MODES, (k, rel_err(got[k], ref[k]))
+
+
+@pytest.mark.parametrize("nc,nf", [(256, 256), (180, 200), (100, 128), (40, 64)])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 0.5), ("cube", 1.0)])
+def test_multi_try_int8_vs_oracle_and_f64(pa, po, rng, nc, nf, dens):
+    """The non-orthogonal one-pass line search with Y and Z = D·W on the int8 digit stage
+    (k_multi_loss2_oz): Σℓ, Σy² of every Y + α_j·Z against the oracle at W + α_j·Z (1e-12,
+    the per-try rounding) and against the fp64-stage pass (1e-13)."""
+    x = laplace_mix(rng, nf, 7001)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    w = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    z = 0.3 * rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    al = np.array([0.5 ** j for j in range(9)])
+    ll, y2 = ctx.eval_loss_multi(w, z, al, mu, d)
+    assert ctx.int8_passes >= 1
+    for j in (0, 4, 8):
+        want = po.pass_stats(w + al[j] * z, mu, x, density_of(po, d), True)
+        assert rel_err(ll[j], want["ll"]) <= TOL and rel_err(y2[j], want["y2"]) <= TOL, j
+    ctx.set_y_stage("f64")
+    n8 = ctx.int8_passes
+    ll64, y264 = ctx.eval_loss_multi(w, z, al, mu, d)
+    assert ctx.int8_passes == n8
+    assert rel_err(ll, ll64) <= TOL_MODES and rel_err(y2, y264) <= TOL_MODES
