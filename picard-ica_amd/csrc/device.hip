@@ -2149,92 +2149,137 @@ __global__ void __launch_bounds__(256) k_moments4(const double* __restrict__ Y, 
 // that moment is the Gram entry of ROW pair (a, b) and COLUMN pair (c, d) with
 // b ≤ c. So rows are ordered by their larger index (R: (a, b) ↦ b(b+1)/2 + a),
 // columns by their smaller one (C: (c, d) ↦ c·n − c(c−1)/2 + d − c), and only the
-// 128 × 128 (R, C) tiles that hold some b ≤ c are computed — 76 of the 289 at
-// n = 64, against 153 for the symmetric upper triangle; k_moments4_fill then
-// gathers the full lexicographic M the host expects.
-// 1D grid: block = tile·nsplit + split. Per 16-sample sub-block: the nc Y rows
-// land in LDS by LDS-DMA two sub-blocks ahead (segments XOR-swizzled per row so
-// the pair gathers below hit distinct banks), each thread forms 8 pair products
-// (masked past cn) into the MFMA A/B fragment image of the NEXT sub-block while
-// the waves run the MFMAs of this one (images double-buffered): one barrier per
-// sub-block. Wave (gi, gj) accumulates a 64 × 32 patch; slab s holds split s's
-// partial tile (summed in fixed order by k_moments4_reduce).
-__device__ __forceinline__ int m4_ys(int row, int t) {  // LDS index of Y(row, t) in a [64][16] sub-block
-  return row * 16 + ((((t >> 1) ^ (row & 7))) << 1) + (t & 1);
+// 64 × 32 (R, C) patches that hold some b ≤ c are computed — 426 of them at
+// n = 64, 0.87 M Gram entries for the 0.77 M distinct moments (the symmetric
+// upper triangle would be 2.2 M); k_moments4_fill then gathers the full
+// lexicographic M the host expects.
+// One patch per wave, any 8 patches per workgroup (a "pack"): every wave forms
+// its own A/B fragments — pair products y_a·y_b of its 64 rows and 32 columns —
+// in registers from the Y stage in LDS, so the waves share nothing but the
+// stage. Per 64-sample stage: the nc ≤ 64 Y rows land in LDS by LDS-DMA one
+// stage ahead (layout [4 sub-blocks][64 rows][16], 16-B segments XOR-swizzled
+// by row so the 16 rows of a fragment hit distinct banks), then 16 k-steps of
+// 8 MFMAs per wave; one barrier per stage. Samples past cn read zeros (the
+// caller zero-pads the chunk to a multiple of 64).
+// XCD-aware grid: block b runs on XCD b % 8 (round-robin dispatch), item
+// (b % 8)·per_xcd + b / 8 ↦ (split, pack) split-major, so the ~32 workgroups an
+// XCD runs at once are mostly packs of ONE split streaming the same Y range in
+// lockstep — the XCD's L2 serves the re-reads. Slab s holds split s's partial
+// Gram (summed in fixed order by k_moments4_reduce).
+// LDS index of Y(row, t) in a [64][16] sub-block: rows are 128 B (32 banks), so rows
+// r and r + 2 share banks; segment s of row r sits at slot s ^ ((r >> 1) & 7), which
+// gives 16 consecutive rows at one t 16 distinct 8-B bank pairs
+__device__ __forceinline__ int m4_ys(int row, int t) {
+  return row * 16 + ((((t >> 1) ^ ((row >> 1) & 7))) << 1) + (t & 1);
+}
+constexpr int M4_STAGE = 64;                       // samples per stage
+constexpr int M4_STAGE_DBL = 64 * M4_STAGE;        // doubles per stage buffer
+constexpr int M4_PACK = FUSED_THREADS / 64;        // patches (waves) per workgroup
+// One 64-sample stage of k_moments4_patch for one wave: 16 k-steps of 8 MFMAs, the 12
+// Y operands of k-step kk + 1 read from LDS while the MFMAs of kk run. The buffer and
+// sub-block offsets are compile-time, so every read is the per-lane row offset plus
+// an immediate.
+template <int CUR>
+__device__ __forceinline__ void m4_stage(const double* smem, const int (&off)[4][12], d4 (&acc)[4][2]) {
+  const double* ys = smem + CUR * M4_STAGE_DBL;
+  double y[12];
+#pragma unroll
+  for (int r = 0; r < 12; ++r) y[r] = ys[off[0][r]];
+#pragma unroll
+  for (int kk = 0; kk < M4_STAGE / 4; ++kk) {
+    double a[4], b[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = y[2 * i] * y[2 * i + 1];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = y[8 + 2 * j] * y[9 + 2 * j];
+    if (kk + 1 < M4_STAGE / 4) {
+      const double* sb = ys + ((kk + 1) >> 2) * 1024;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) y[r] = sb[off[(kk + 1) & 3][r]];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);  // keep each k-step's reads with its MFMAs
+  }
 }
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
-k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc, const int* __restrict__ ri,
-                const int* __restrict__ rj, const int* __restrict__ ci, const int* __restrict__ cj, int np,
-                const int* __restrict__ tile_p, const int* __restrict__ tile_q, int nsplit, uint64_t spb,
-                double* __restrict__ slabs, size_t slab_stride) {
+k_moments4_patch(const double* __restrict__ Y, uint64_t ldy, uint64_t n_stage, int nc, const int* __restrict__ ri,
+                 const int* __restrict__ rj, const int* __restrict__ ci, const int* __restrict__ cj, int np,
+                 const int* __restrict__ packs, int npack, int nsplit, uint64_t spb, uint64_t per_xcd,
+                 double* __restrict__ slabs, size_t slab_stride) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
-  const int tile = blockIdx.x / nsplit, split = blockIdx.x % nsplit;
-  const int tp = tile_p[tile], tq = tile_q[tile];
-  const int gi0 = (wave >> 2) * 4, gj0 = (wave & 3) * 2;
-  extern __shared__ double smem[];
-  double* ys0 = smem;              // [2][64][16] Y sub-blocks (swizzled)
-  double* zf0 = smem + 2 * 1024;   // [2][2 (P, Q)][8 pair blocks][4 k-steps][64 lanes]
+  const uint64_t item = (uint64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int split = (int)(item / npack), pack = (int)(item % npack);
+  if (split >= nsplit) return;  // padding item (uniform over the workgroup)
+  const int pat = packs[pack * M4_PACK + wave];
+  const bool active = pat >= 0;
+  const int g = active ? pat >> 16 : 0, h = active ? pat & 0xffff : 0;
+  extern __shared__ double smem[];  // [2][M4_STAGE_DBL]
   d4 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = d4{0, 0, 0, 0};
-  // this thread's 8 products per sub-block: element e = tid + 512·u of the
-  // [2][8][4][64] fragment image → pair (set, block, lane&15), sample 4·kk + lane>>4
-  int ia[8], ja[8];
+  // this lane's pair rows: A block i ↦ R pair g·64 + 16i + lr, B block j ↦ C pair h·32 + 16j + lr
+  // (pairs past np use row 0; their entries are never stored)
+  int ra0[4], ra1[4], rb0[2], rb1[2];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = tid + FUSED_THREADS * u;
-    const int set = e >> 11, blk = (e >> 8) & 7, ln = e & 63;
-    const int pr = (set ? tq : tp) * 128 + blk * 16 + (ln & 15);
-    ia[u] = pr < np ? (set ? ci[pr] : ri[pr]) : -1;
-    ja[u] = pr < np ? (set ? cj[pr] : rj[pr]) : -1;
+  for (int i = 0; i < 4; ++i) {
+    const int p = g * 64 + 16 * i + lr;
+    ra0[i] = p < np ? ri[p] : 0;
+    ra1[i] = p < np ? rj[p] : 0;
   }
-  const uint64_t nsb = (cn + 15) / 16;
-  const uint64_t s_begin = (uint64_t)split * spb, s_end = s_begin + spb < nsb ? s_begin + spb : nsb;
-  // LDS-DMA: wave w moves rows 8w … 8w+7 of a sub-block (rows ≥ nc read row 0,
-  // never gathered); lane L → row 8w + L/8, slot L%8 holds segment (L%8) ^ (row%8)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = h * 32 + 16 * j + lr;
+    rb0[j] = q < np ? ci[q] : 0;
+    rb1[j] = q < np ? cj[q] : 0;
+  }
+  const uint64_t s_begin = (uint64_t)split * spb, s_end = s_begin + spb < n_stage ? s_begin + spb : n_stage;
+  // LDS-DMA: instruction u of wave w moves sub-block u, rows 8w … 8w+7 (rows ≥ nc
+  // read row 0, never gathered); lane L → row 8w + L/8, slot L%8 holds segment (L%8) ^ ((row/2)%8)
   const int yrow = 8 * wave + (lane >> 3);
-  const double* ysrc = Y + (size_t)(yrow < nc ? yrow : 0) * ldy + 2 * ((lane & 7) ^ (lane >> 3));
-  auto stage = [&](uint64_t sb, double* ys) {
-    __builtin_amdgcn_global_load_lds((gbl_vptr)(ysrc + sb * 16), (lds_vptr)(ys + wave * 128), 16, 0, 0);
-  };
-  auto products = [&](uint64_t sb, const double* ys, double* zf) {
+  const double* ysrc = Y + (size_t)(yrow < nc ? yrow : 0) * ldy + 2 * ((lane & 7) ^ ((yrow >> 1) & 7));
+  auto stage = [&](uint64_t s, double* ys) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + FUSED_THREADS * u;
-      const int t = 4 * ((e >> 6) & 3) + ((e & 63) >> 4);
-      zf[e] = ia[u] >= 0 && sb * 16 + t < cn ? ys[m4_ys(ia[u], t)] * ys[m4_ys(ja[u], t)] : 0.0;
+    for (int u = 0; u < 4; ++u)
+      __builtin_amdgcn_global_load_lds((gbl_vptr)(ysrc + s * M4_STAGE + 16 * u), (lds_vptr)(ys + u * 1024 + wave * 128),
+                                       16, 0, 0);
+  };
+  // per-lane LDS offsets of the 12 operand rows (A: y_a, y_b of 4 R pairs; B: of 2 C
+  // pairs) at t = 4·kq + lane/16 of a sub-block
+  int off[4][12];
+#pragma unroll
+  for (int kq = 0; kq < 4; ++kq) {
+    const int t = 4 * kq + lk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      off[kq][2 * i] = m4_ys(ra0[i], t);
+      off[kq][2 * i + 1] = m4_ys(ra1[i], t);
     }
-  };
-  if (s_begin < s_end) {
-    stage(s_begin, ys0);
-    if (s_begin + 1 < s_end) stage(s_begin + 1, ys0 + 1024);
-    __syncthreads();
-    products(s_begin, ys0, zf0);
-    __syncthreads();
-    int cur = 0;
-    for (uint64_t sb = s_begin; sb < s_end; ++sb) {
-      if (sb + 2 < s_end) stage(sb + 2, ys0 + cur * 1024);  // Y(sb) was read by the products of the last iteration
-      if (sb + 1 < s_end) products(sb + 1, ys0 + (cur ^ 1) * 1024, zf0 + (cur ^ 1) * 4096);
-      const double* zf = zf0 + cur * 4096;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        double a[4], b[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = zf[((gi0 + i) * 4 + kk) * 64 + lane];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) b[j] = zf[2048 + ((gj0 + j) * 4 + kk) * 64 + lane];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
-      }
-      __syncthreads();  // products of sb + 1 written, this wave's DMA of sb + 2 landed
-      cur ^= 1;
+    for (int j = 0; j < 2; ++j) {
+      off[kq][8 + 2 * j] = m4_ys(rb0[j], t);
+      off[kq][9 + 2 * j] = m4_ys(rb1[j], t);
     }
   }
+  if (s_begin < s_end) {  // stages alternate between the two buffers, two per trip
+    stage(s_begin, smem);
+    __syncthreads();
+    for (uint64_t s = s_begin; s < s_end; s += 2) {
+      if (s + 1 < s_end) stage(s + 1, smem + M4_STAGE_DBL);  // buffer 1 was read last in the previous trip
+      if (active) m4_stage<0>(smem, off, acc);
+      __syncthreads();  // stage s read by every wave, this wave's DMA of s + 1 landed
+      if (s + 1 >= s_end) break;
+      if (s + 2 < s_end) stage(s + 2, smem);
+      if (active) m4_stage<1>(smem, off, acc);
+      __syncthreads();
+    }
+  }
+  if (!active) return;
   double* out = slabs + split * slab_stride;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -2242,18 +2287,18 @@ k_moments4_mfma(const double* __restrict__ Y, uint64_t ldy, uint64_t cn, int nc,
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int p = tp * 128 + (gi0 + i) * 16 + lk + 4 * r, q = tq * 128 + (gj0 + j) * 16 + lr;
+        const int p = g * 64 + 16 * i + lk + 4 * r, q = h * 32 + 16 * j + lr;
         if (p < np && q < np) out[(size_t)p * np + q] = acc[i][j][r];
       }
 }
 
-// acc[p][q] (+)= Σ_s slabs[s][p][q] over the (R, C) tiles k_moments4_mfma computed
+// acc[p][q] (+)= Σ_s slabs[s][p][q] over the 64 × 32 (R, C) patches k_moments4_patch computed
 __global__ void k_moments4_reduce(const double* __restrict__ slabs, int nsplit, size_t slab_stride, int np,
-                                  const unsigned char* __restrict__ tmask, int accumulate, double* __restrict__ acc) {
+                                  const unsigned char* __restrict__ pmask, int accumulate, double* __restrict__ acc) {
   const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (e >= (size_t)np * np) return;
-  const int p = (int)(e / np), q = (int)(e % np), nt = (np + 127) / 128;
-  if (!tmask[(p / 128) * nt + q / 128]) return;
+  const int p = (int)(e / np), q = (int)(e % np), nqc = (np + 31) / 32;
+  if (!pmask[(p / 64) * nqc + q / 32]) return;
   double s = 0.0;
   for (int k = 0; k < nsplit; ++k) s += slabs[k * slab_stride + e];
   acc[e] = accumulate ? acc[e] + s : s;
@@ -3808,8 +3853,7 @@ struct DeviceCtx : Evaluator {
     ystore_upload(w, nc, nf);
     const bool mfma_path = nc <= 64;  // larger nc: the VALU tile kernel (symmetric upper tiles)
     const uint64_t CH = mfma_path ? (1ull << 22) : (1ull << 16);
-    const int nt = (np + 127) / 128;
-    // (R, C) pair orders and the staircase tiles of k_moments4_mfma
+    // (R, C) pair orders and the staircase patches of k_moments4_patch
     std::vector<int> ri(np), rj(np), ci(np), cj(np);
     {
       int q = 0;
@@ -3819,23 +3863,33 @@ struct DeviceCtx : Evaluator {
       for (int c = 0; c < (int)nc; ++c)
         for (int d = c; d < (int)nc; ++d) { ci[q] = c; cj[q] = d; ++q; }
     }
-    std::vector<int> tpv, tqv;
-    std::vector<unsigned char> tmask((size_t)nt * nt, 0);
-    for (int a = 0; a < nt; ++a) {
-      int bmin = INT_MAX;
-      for (int r = a * 128; r < std::min(np, a * 128 + 128); ++r) bmin = std::min(bmin, rj[r]);
-      for (int b = 0; b < nt; ++b) {
-        int cmax = -1;
-        for (int c = b * 128; c < std::min(np, b * 128 + 128); ++c) cmax = std::max(cmax, ci[c]);
-        if (bmin <= cmax) { tpv.push_back(a); tqv.push_back(b); tmask[(size_t)a * nt + b] = 1; }
+    const int nrg = (np + 63) / 64, nqc = (np + 31) / 32;
+    std::vector<int> packs;
+    std::vector<unsigned char> pmask((size_t)nrg * nqc, 0);
+    for (int g = 0; g < nrg; ++g) {
+      const int bmin = rj[g * 64];  // rows are ordered by b
+      for (int h = 0; h < nqc; ++h) {
+        const int cmax = ci[std::min(np, h * 32 + 32) - 1];  // columns by c
+        if (bmin <= cmax) { packs.push_back(g << 16 | h); pmask[(size_t)g * nqc + h] = 1; }
       }
     }
-    const int ntile = (int)tpv.size();
-    // ≈ three whole rounds of one workgroup per CU
-    const int nsplit = mfma_path ? std::max(1, (int)std::lround(3.0 * n_cu / ntile)) : 1;
+    while (packs.size() % M4_PACK) packs.push_back(-1);  // idle waves
+    const int npack = (int)(packs.size() / M4_PACK);
+    // splits: the item count (npack · nsplit) that fills whole rounds of one workgroup
+    // per CU best, at ≥ 2 rounds
+    int nsplit = 1;
+    if (mfma_path) {
+      double best = -1;
+      for (int s = 1; s <= 48; ++s) {
+        const double items = (double)npack * s, rounds = std::ceil(items / n_cu);
+        if (rounds < 2) continue;
+        const double fill = items / (rounds * n_cu);
+        if (fill > best + 1e-9) { best = fill; nsplit = s; }
+      }
+    }
     const size_t slab_stride = (size_t)np * np;
     auto dsz = [](size_t bytes) { return (bytes + sizeof(double) - 1) / sizeof(double); };
-    const size_t ints = dsz((6 * (size_t)np + 2 * (size_t)ntile) * sizeof(int) + (size_t)nt * nt);
+    const size_t ints = dsz((6 * (size_t)np + packs.size()) * sizeof(int) + pmask.size());
     const size_t need = nc * CH + (mfma_path ? 2 : 1) * (size_t)np * np + ints + (mfma_path ? nsplit * slab_stride : 0);
     double* Y = ensure(d_chunk, cap_chunk, need);
     double* acc = Y + nc * CH;
@@ -3846,9 +3900,8 @@ struct DeviceCtx : Evaluator {
     int* drj = dri + np;
     int* dci = drj + np;
     int* dcj = dci + np;
-    int* dtp = dcj + np;
-    int* dtq = dtp + ntile;
-    unsigned char* dtm = reinterpret_cast<unsigned char*>(dtq + ntile);
+    int* dpk = dcj + np;
+    unsigned char* dtm = reinterpret_cast<unsigned char*>(dpk + packs.size());
     double* slabs = full + (size_t)np * np + ints;
     HIP_OK(hipMemcpyAsync(dpi, pi.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dpj, pj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
@@ -3856,9 +3909,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(drj, rj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dci, ci.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemcpyAsync(dcj, cj.data(), np * sizeof(int), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(dtp, tpv.data(), ntile * sizeof(int), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(dtq, tqv.data(), ntile * sizeof(int), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(dtm, tmask.data(), tmask.size(), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dpk, packs.data(), packs.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(dtm, pmask.data(), pmask.size(), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemsetAsync(acc, 0, (size_t)np * np * sizeof(double), stream));
     // the host image vectors must outlive the async copies
     sync();
@@ -3868,12 +3920,16 @@ struct DeviceCtx : Evaluator {
       const uint64_t cn = std::min<uint64_t>(CH, n_local_ - c0);
       ystore_run(X + c0, ldx, nf, nc, cn, Y, CH);
       if (mfma_path) {
-        const uint64_t nsb = (cn + 15) / 16;
-        const uint64_t spb = (nsb + nsplit - 1) / nsplit;
-        const size_t lds = (size_t)(2 * 64 * 16 + 2 * 2 * 8 * 4 * 64) * sizeof(double);
-        lds_attr((const void*)k_moments4_mfma, (int)lds);
-        k_moments4_mfma<<<(unsigned)(ntile * nsplit), FUSED_THREADS, lds, stream>>>(
-            Y, CH, cn, (int)nc, dri, drj, dci, dcj, np, dtp, dtq, nsplit, spb, slabs, slab_stride);
+        const uint64_t n_stage = (cn + M4_STAGE - 1) / M4_STAGE;
+        if (cn % M4_STAGE)  // the last stage reads zeros past cn (CH is a multiple of M4_STAGE)
+          HIP_OK(hipMemset2DAsync(Y + cn, CH * sizeof(double), 0, (n_stage * M4_STAGE - cn) * sizeof(double), nc,
+                                  stream));
+        const uint64_t spb = (n_stage + nsplit - 1) / nsplit;
+        const uint64_t per_xcd = ((uint64_t)npack * nsplit + 7) / 8;
+        const size_t lds = (size_t)2 * M4_STAGE_DBL * sizeof(double);
+        lds_attr((const void*)k_moments4_patch, (int)lds);
+        k_moments4_patch<<<(unsigned)(8 * per_xcd), FUSED_THREADS, lds, stream>>>(
+            Y, CH, n_stage, (int)nc, dri, drj, dci, dcj, np, dpk, npack, nsplit, spb, per_xcd, slabs, slab_stride);
         HIP_OK(hipGetLastError());
         k_moments4_reduce<<<(unsigned)(((size_t)np * np + 255) / 256), 256, 0, stream>>>(slabs, nsplit, slab_stride, np,
                                                                                          dtm, first ? 0 : 1, acc);
