@@ -3320,7 +3320,8 @@ struct DeviceCtx : Evaluator {
     if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
     if (oz_kso() != KSO) throw computation_error("int8 digit image of another layout");
     const size_t lds = (size_t)2 * 2 * (oz_block_bytes<KSO>() + 256) + (size_t)2 * 2 * 8 * 4 * 64 * sizeof(double);
-    auto kern = F32L ? k_eval_loss_oz<D, false, Q, DMAX, F32L, NB>
+    auto kern = F32L ? (oz_pair_ ? k_eval_loss_oz<D, false, Q, DMAX, F32L, NB>
+                                 : k_eval_loss_oz<D, false, Q, DMAX, F32L, NB, false>)
                      : store ? k_eval_loss_oz<D, true, Q, DMAX, false, NB> : k_eval_loss_oz<D, false, Q, DMAX, false, NB>;
     lds_attr((const void*)kern, (int)lds);
     HIP_OK(hipEventRecord(ev[1], stream));
@@ -3335,7 +3336,8 @@ struct DeviceCtx : Evaluator {
     if (DMAX < OZ_SLICES - 1) ++n_screen_passes_;
   }
   uint64_t n_screen_passes_ = 0;
-  bool no_ws4_ = std::getenv("PICARD_NO_WS4") != nullptr;
+  bool oz_pair_ = std::getenv("PICARD_OZ_NOPAIR") == nullptr;  // A/B knob: paired M-wave blocks
+  bool no_ws4_ =std::getenv("PICARD_NO_WS4") != nullptr;
   // the tanh screen evaluates ℓ in fp32 (PICARD_SCREEN_F64=1: the fp64 row terms of the
   // exact pass, a tighter bound at a higher cost)
   bool screen_f32_ = std::getenv("PICARD_SCREEN_F64") == nullptr;

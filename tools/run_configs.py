@@ -1,5 +1,5 @@
 """Run BASELINE configs end-to-end on one GPU (device-generated bench mixture).
-Usage: python tools/run_configs.py C2 [C4 C5 ...] [--oracle] [--max-iter=K]  → one JSON line per config."""
+Usage: python tools/run_configs.py C2 [C4 C5 ...] [--oracle] [--max-iter=K] [--maps=PATH]  → one JSON line per config."""
 import json
 import os
 import sys
@@ -42,6 +42,7 @@ def run(name, oracle=False, max_iter=None):
            "samples_per_s_per_iter": t * r.n_iterations / t_iter,
            "amari": pa.utils.amari_distance(r.full_unmixing(), a),
            "kernels": {k: v for k, v in ctx.kernel_breakdown().items()}}
+    s.close()
     if oracle:
         from oracle import picard_oracle as po
         x = ctx.download()
@@ -51,6 +52,7 @@ def run(name, oracle=False, max_iter=None):
         out["oracle_s"] = time.perf_counter() - t2
         out["oracle_amari"] = po.amari_distance(ro.full_unmixing(), a)
         out["oracle_n_iterations"] = ro.n_iterations
+    ctx.close()
     print(json.dumps(out), flush=True)
 
 
@@ -73,3 +75,4 @@ if __name__ == "__main__":
     mi = [int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--max-iter=")]
     for name in [a for a in sys.argv[1:] if not a.startswith("--")]:
         run(name, want_oracle, mi[0] if mi else None)
+
