@@ -34,6 +34,8 @@ namespace pcamd {
 size_t jade_max_pairs();  // host_solver.cpp (PICARD_JADE_MAX_PAIRS test hook)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 // LDS-DMA (global_load_lds) operand address spaces
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef __attribute__((address_space(1))) void* gbl_vptr;
@@ -435,6 +437,23 @@ __device__ __forceinline__ void loss_acc4_f32(const d4& y, float c32, RowAcc& a)
     pf *= __builtin_fmaf(__builtin_amdgcn_exp2f(z), 0.5f, 0.5f);
   }
   a.g += (double)__builtin_amdgcn_logf(pf);
+}
+
+// The same ℓ terms from the M waves' fp32 |ỹ| (k_eval_loss_oz, F32L): Σ|ỹ| of the 4 in fp32
+// ((a0 + a2) + (a1 + a3): ≤ 2^-23·Σ relative) into the fp64 sum, z = ỹ·c32 (2 roundings: within
+// the 3.0000002·2^-24 of screen_f32_block_bound), the rest as loss_acc4_f32; pairs of lanes go
+// through the packed fp32 ops.
+__device__ __forceinline__ void loss_acc4_f32y(const f4& y, float c32, RowAcc& a) {
+  const f2 lo = {y[0], y[1]}, hi = {y[2], y[3]};
+  const f2 s2 = lo + hi;
+  a.l += (double)(s2[0] + s2[1]);
+  const f2 zl = lo * c32, zh = hi * c32;
+  f2 el = {__builtin_amdgcn_exp2f(zl[0]), __builtin_amdgcn_exp2f(zl[1])};
+  f2 eh = {__builtin_amdgcn_exp2f(zh[0]), __builtin_amdgcn_exp2f(zh[1])};
+  el = el * 0.5f + 0.5f;
+  eh = eh * 0.5f + 0.5f;
+  const f2 p2 = el * eh;
+  a.g += (double)__builtin_amdgcn_logf(p2[0] * p2[1]);
 }
 
 // every ≤ 32 blocks (≤ 128 factors ∈ (1, 2] since the last call: no overflow);
@@ -1136,6 +1155,28 @@ __device__ __forceinline__ double reduce_partials(const double* __restrict__ p, 
   red[g][o] = s;
   __syncthreads();
   return (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
+}
+
+// min, max and a NaN flag of the n sample scales 2^e_t, per workgroup: out[3·b + {0, 1, 2}]
+__global__ void __launch_bounds__(256) k_xsc_range(const double* __restrict__ xsc, uint64_t n, double* __restrict__ out) {
+  __shared__ double s[3][256];
+  double lo = INFINITY, hi = 0.0, nan = 0.0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const double v = xsc[i];
+    if (v != v) nan = 1.0;
+    else { lo = fmin(lo, v); hi = fmax(hi, v); }
+  }
+  s[0][threadIdx.x] = lo; s[1][threadIdx.x] = hi; s[2][threadIdx.x] = nan;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      s[0][threadIdx.x] = fmin(s[0][threadIdx.x], s[0][threadIdx.x + h]);
+      s[1][threadIdx.x] = fmax(s[1][threadIdx.x], s[1][threadIdx.x + h]);
+      s[2][threadIdx.x] = fmax(s[2][threadIdx.x], s[2][threadIdx.x + h]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) out[3 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
 }
 
 // out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets,
@@ -2445,7 +2486,16 @@ struct DeviceCtx : Evaluator {
   // issued asynchronously and an event after it guards the slot — the next writer of the
   // slot waits on that event, so no stream synchronisation follows the upload.
   struct PinSlot { void* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
-  PinSlot pin_w_, pin_wsl_;
+  PinSlot pin_w_, pin_wsl_, pin_out_, pin_in_;
+  // D2H of n doubles through the pinned out slot (a DMA copy; a pageable destination takes a
+  // staging blit and a blocking copy): enqueue now, copy_out() after the stream has synced
+  const double* d2h_enqueue(const double* dsrc, size_t n) {
+    double* h = (double*)pin_acquire(pin_out_, std::max<size_t>(n, 1) * sizeof(double));
+    HIP_OK(hipMemcpyAsync(h, dsrc, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+    pin_release(pin_out_);
+    return h;
+  }
+  static void copy_out(double* dst, const double* staged, size_t n) { std::memcpy(dst, staged, n * sizeof(double)); }
   void* pin_acquire(PinSlot& sl, size_t bytes) {
     if (sl.pending) {
       HIP_OK(hipEventSynchronize(sl.ev));
@@ -2488,7 +2538,7 @@ struct DeviceCtx : Evaluator {
     for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsl, (void*)d_wsc})
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (PinSlot* sl : {&pin_w_, &pin_wsl_}) {
+    for (PinSlot* sl : {&pin_w_, &pin_wsl_, &pin_out_, &pin_in_}) {
       if (sl->pending) (void)hipEventSynchronize(sl->ev);
       if (sl->p) (void)hipHostFree(sl->p);
       if (sl->ev) (void)hipEventDestroy(sl->ev);
@@ -2846,9 +2896,10 @@ struct DeviceCtx : Evaluator {
       throw computation_error("no evaluation path for density id " + std::to_string(dens));
     }
     allreduce(st, total, need_h ? "eval+H" : "eval");
-    HIP_OK(hipMemcpyAsync(stats_host, st, total * sizeof(double), hipMemcpyDeviceToHost, stream));
+    const double* staged = d2h_enqueue(st, total);
     HIP_OK(hipEventRecord(ev[3], stream));
     sync();
+    copy_out(stats_host, staged, total);
     float a = 0, b = 0;
     const bool timed = fused || tiled;  // "fused" kind = every full pass (fused or tiled)
     if (timed) { HIP_OK(hipEventElapsedTime(&a, ev[1], ev[2])); }
@@ -2978,8 +3029,9 @@ struct DeviceCtx : Evaluator {
   void multi_finish(double* st, size_t nc, int na, double* ll_out, double* y2_out) {
     allreduce(st, (size_t)2 * na * nc, "loss_multi");
     std::vector<double> h((size_t)2 * na * nc);
-    HIP_OK(hipMemcpyAsync(h.data(), st, h.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
+    const double* staged = d2h_enqueue(st, h.size());
     finish_timing(true, 3);
+    copy_out(h.data(), staged, h.size());
     for (int j = 0; j < na; ++j) {
       std::memcpy(ll_out + (size_t)j * nc, h.data() + (size_t)(j * 2 + 0) * nc, nc * sizeof(double));
       std::memcpy(y2_out + (size_t)j * nc, h.data() + (size_t)(j * 2 + 1) * nc, nc * sizeof(double));
@@ -3216,7 +3268,7 @@ struct DeviceCtx : Evaluator {
     if (xsl_failed_ || nf > 256) return false;
     // the scratch of the Σ 2^e_t sum first: an allocation here may release the image
     const int nwg_e = (int)std::max<uint64_t>(1, std::min<uint64_t>((ldx + 4095) / 4096, 1024));
-    ensure(d_shift_part, cap_shift_part, (size_t)nwg_e + 1);
+    ensure(d_shift_part, cap_shift_part, std::max<size_t>((size_t)nwg_e + 1, 3 * (size_t)std::min(nwg_e, 256)));
     if (xsl_failed_) return false;
     const uint64_t n_blocks = ldx / 16;
     const size_t need = (size_t)n_blocks * oz_bb();
@@ -3251,11 +3303,35 @@ struct DeviceCtx : Evaluator {
       HIP_OK(hipGetLastError());
       HIP_OK(hipMemcpyAsync(&xsc_sum_, part + nwg, sizeof(double), hipMemcpyDeviceToHost, stream));
       sync();
+      // min / max of 2^e_t (part is free again: NaN scales make the range unusable)
+      const int nr = (int)std::min<uint64_t>(nwg, 256);
+      k_xsc_range<<<nr, 256, 0, stream>>>(d_xsc, ldx, part);
+      HIP_OK(hipGetLastError());
+      std::vector<double> mm(3 * (size_t)nr);
+      HIP_OK(hipMemcpyAsync(mm.data(), part, mm.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
+      sync();
+      double lo = INFINITY, hi = 0.0;
+      bool nan = false;
+      for (int b = 0; b < nr; ++b) {
+        lo = std::min(lo, mm[3 * b]);
+        hi = std::max(hi, mm[3 * b + 1]);
+        nan |= mm[3 * b + 2] != 0.0;
+      }
+      xsc_range_ok_ = !nan && lo > 0.0 && std::isfinite(hi);
+      if (xsc_range_ok_) {
+        (void)std::frexp(lo, &xsc_emin_);
+        (void)std::frexp(hi, &xsc_emax_);
+        xsc_emin_ -= 1;  // 2^e = 0.5·2^(e+1): frexp gives e + 1
+        xsc_emax_ -= 1;
+      }
     }
     xsl_valid_ = true;
     return true;
   }
   double xsc_sum_ = 0.0;
+  // exponent range of the digit image's sample scales 2^e_t (the fp32 screen's range check)
+  int xsc_emin_ = 0, xsc_emax_ = 0;
+  bool xsc_range_ok_ = false;
   // W (nc × nf, host) → slice image [wave][a][kstep][lane][16 B] + row scales 2^(f_i − 12).
   // The same W as the last call (a completion at the W of the loss-only try) is not
   // sliced again. Digits: oz_digits' arithmetic with a 1.5·2^52 shifter for rint
@@ -3431,7 +3507,7 @@ struct DeviceCtx : Evaluator {
     const bool nb4 = oz4_shape(nc);
     HIP_OK(hipSetDevice(device));
     const double* dmu = resident_mu(mu);
-    double* st_rows = ensure(d_stats, cap_stats, 2 * nc);
+    double* st_rows = ensure(d_stats, cap_stats, 3 * nc);  // [Σℓ | Σ|ỹ| (fp32 screen) | bound]
     {  // the pass buffers before the image is relied on (an allocation may release it)
       uint64_t bpw0;
       const int nwg0 = partition(nb4 ? (n_local_ + 31) / 32 : (n_local_ + 15) / 16, &bpw0);
@@ -3446,47 +3522,62 @@ struct DeviceCtx : Evaluator {
     upload_wsl(w, nc);
     d_wsl_ready_ = true;
     kept_nc_pending = nc;
-    HIP_OK(hipEventRecord(ev[0], stream));
-    const bool f32l = d.kind == DENS_TANH && screen_f32_;
-    if (nb4) screen_launch<4>(d, dmax, f32l, st_rows);
-    else screen_launch<8>(d, dmax, f32l, st_rows);
-    // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
-    double bsum = 0.0;
-    for (int dd = dmax + 1; dd <= 2 * (OZ_SLICES - 1); ++dd) {
-      double pm = 0.0;
-      for (int a = 0; a < OZ_SLICES; ++a) {
-        const int b = dd - a;
-        if (b < 0 || b >= OZ_SLICES) continue;
-        pm += (a == 0 ? 65.0 : 128.0) * (b == 0 ? 65.0 : 128.0);
-      }
-      if (dd <= OZ_SLICES - 1) bsum += std::ldexp(pm, -8 * dd);  // only D ≤ 6 are in the exact stage
-    }
-    const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
-    const double tail = (double)nf * bsum * xsc_sum_ * lip;
-    std::vector<double> bnd(nc);
+    // W row exponents (the kernels' f_i: 2^f_i > max_k |W_ik|; 0 for a zero row)
+    std::vector<int> fexp(nc, 0);
+    std::vector<char> zero_row(nc, 1);
     for (size_t i = 0; i < nc; ++i) {
       double mx = 0.0;
       for (size_t k = 0; k < nf; ++k) {
         const double f = std::fabs(w[i * nf + k]);
         mx = f > mx ? f : mx;  // = fmax: a NaN weight is skipped, as fmax skips it
       }
-      int e = 0;
-      if (mx > 0.0) (void)std::frexp(mx, &e);
-      bnd[i] = std::ldexp(tail, e - 12) * (1.0 + 1e-12);
+      if (mx > 0.0) { (void)std::frexp(mx, &fexp[i]); zero_row[i] = 0; }
+    }
+    // fp32 screen (tanh): every scale 2^(f_i+e_t−20) a normal fp32 power of two with room for
+    // |Q01| < 2^28 above it and 2^-24 below it (else this rank runs the fp64-ℓ screen: both
+    // issue the same all-reduce and each rank's part of the bound covers its own arithmetic)
+    bool f32l = d.kind == DENS_TANH && screen_f32_ && xsc_range_ok_;
+    for (size_t i = 0; f32l && i < nc; ++i)
+      if (!zero_row[i] && (fexp[i] - 20 + xsc_emin_ < -100 || fexp[i] - 20 + xsc_emax_ > 99)) f32l = false;
+    HIP_OK(hipEventRecord(ev[0], stream));
+    if (nb4) screen_launch<4>(d, dmax, f32l, st_rows);
+    else screen_launch<8>(d, dmax, f32l, st_rows);
+    // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
+    auto pm = [](int dd) {  // Σ_{a+b=dd} |d_a|max·|d_b|max per feature
+      double v = 0.0;
+      for (int a = 0; a < OZ_SLICES; ++a) {
+        const int b = dd - a;
+        if (b >= 0 && b < OZ_SLICES) v += (a == 0 ? 65.0 : 128.0) * (b == 0 ? 65.0 : 128.0);
+      }
+      return v;
+    };
+    double bsum = 0.0;
+    for (int dd = dmax + 1; dd <= OZ_SLICES - 1; ++dd) bsum += std::ldexp(pm(dd), -8 * dd);  // exact stage: D ≤ 6
+    // fp32 combine (oz_combine_screen_f32): the absolute part 2^-38·(|R23| + |P_4|/256)·2^(f_i+e_t−20)
+    if (f32l) bsum += std::ldexp(256.0 * pm(2) + pm(3) + pm(4) / 256.0, -46) * (1.0 + 1e-6);
+    const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
+    const double tail = (double)nf * bsum * xsc_sum_ * lip;
+    double* bnd = (double*)pin_acquire(pin_in_, nc * sizeof(double));  // H2D by DMA
+    for (size_t i = 0; i < nc; ++i) {
+      bnd[i] = std::ldexp(tail, fexp[i] - 12) * (1.0 + 1e-12);
       // fp32 ℓ: 4 lane-blocks of 4 samples per 16-sample block of this row (padding included)
       if (f32l) bnd[i] += (double)(ldx / 4) * screen_f32_block_bound(d.alpha);
     }
-    HIP_OK(hipMemcpyAsync(st_rows + nc, bnd.data(), nc * sizeof(double), hipMemcpyHostToDevice, stream));
-    allreduce(st_rows, 2 * nc, "screen");
-    std::vector<double> tmp(2 * nc);
-    HIP_OK(hipMemcpyAsync(tmp.data(), st_rows, 2 * nc * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(st_rows + 2 * nc, bnd, nc * sizeof(double), hipMemcpyHostToDevice, stream));
+    pin_release(pin_in_);
+    allreduce(st_rows, 3 * nc, "screen");
+    std::vector<double> tmp(3 * nc);
+    const double* staged = d2h_enqueue(st_rows, 3 * nc);
     finish_timing(true, 4);
-    // the rounding slack: Σ_t |ℓ| ≤ |Σℓ| for tanh (ℓ ≥ 0), ≤ n/α for exp (|ℓ| ≤ 1/α)
-    const double n_all = (double)n_total;
+    copy_out(tmp.data(), staged, 3 * nc);
+    // the rounding slack: Σ_t |ℓ| ≤ |Σℓ| for tanh (ℓ ≥ 0), ≤ n/α for exp (|ℓ| ≤ 1/α);
+    // fp32 screen: κ1·Σ|ỹ| covers |ỹ| against the DMAX-digit y and the fp32 sum of |ỹ|
+    // (slot 1 is Σ|ỹ| on the ranks that ran it, 0 on the others: the kernels' Σy² is not kept)
+    const double n_all = (double)n_total, kappa1 = 0x1p-22 * 1.0001;
     for (size_t i = 0; i < nc; ++i) {
       ll_out[i] = tmp[i];
       const double abs_l = d.kind == DENS_TANH ? std::fabs(tmp[i]) : n_all / d.alpha;
-      bound_out[i] = tmp[nc + i] + 1e-10 * abs_l;
+      bound_out[i] = tmp[2 * nc + i] + kappa1 * std::fabs(tmp[nc + i]) + 1e-10 * abs_l;
     }
     return true;
   }
@@ -3610,9 +3701,9 @@ struct DeviceCtx : Evaluator {
       tiled_eval(w, nc, dmu, d.kind, d.alpha, need_h, st, 1);
       HIP_OK(hipEventRecord(ev[2], stream));
       allreduce(st + total - 2 * nc, 2 * nc, "loss");
-      HIP_OK(hipMemcpyAsync(out->buf.data() + total - 2 * nc, st + total - 2 * nc, 2 * nc * sizeof(double),
-                            hipMemcpyDeviceToHost, stream));
+      const double* staged = d2h_enqueue(st + total - 2 * nc, 2 * nc);
       finish_timing(true, 1);
+      copy_out(out->buf.data() + total - 2 * nc, staged, 2 * nc);
       kept_tiled = true;
       kept_nc = nc;
       kept_w.assign(w, w + nc * nf);
@@ -3666,9 +3757,9 @@ struct DeviceCtx : Evaluator {
     }
 #undef PC_LOSS
     allreduce(st_rows, 2 * nc, "loss");
-    HIP_OK(hipMemcpyAsync(out->buf.data() + total - 2 * nc, st_rows, 2 * nc * sizeof(double),
-                          hipMemcpyDeviceToHost, stream));
+    const double* staged = d2h_enqueue(st_rows, 2 * nc);
     finish_timing(true, 1);
+    copy_out(out->buf.data() + total - 2 * nc, staged, 2 * nc);
     kept_nc = nc;
     kept_nb = nb;
     kept_tiled = !store;  // "recompute" completion
@@ -3735,8 +3826,9 @@ struct DeviceCtx : Evaluator {
       default: dispatch_fromy<8>(d, need_h, st); break;
     }
     allreduce(st, e1, need_h ? "complete+H" : "complete");
-    HIP_OK(hipMemcpyAsync(out->buf.data(), st, e1 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    const double* staged = d2h_enqueue(st, e1);
     finish_timing(true, 2);
+    copy_out(out->buf.data(), staged, e1);
   }
 
   void sources(const double* w, size_t nc, const double* mu, double* out) override {

@@ -63,3 +63,27 @@ def test_f32_screen_bound_covers_exact(pa, n, alpha, dmax, monkeypatch):
         assert np.all(b32 >= b64)  # the fp32 bound adds to the digit tail
         tight = 1e-4 if dmax == "3" else 1e-5  # the dropped digit diagonals dominate the bound
         assert np.max(b32 / np.abs(exact)) <= tight, (scale, np.max(b32 / np.abs(exact)))
+
+
+@pytest.mark.parametrize("tiny", [1e-35, 1e-25])
+def test_f32_screen_scale_range(pa, tiny):
+    """The fp32 screen forms |ỹ| = |Y'|·2^(f_i+e_t−20) in fp32, which needs every scale in the
+    normal fp32 range (DeviceCtx::screen_at checks the digit image's exponent range): a sample
+    of size 1e-35 takes the rank to the fp64-ℓ screen, one of 1e-25 keeps the fp32 screen; the
+    bound covers the exact pass either way."""
+    rng = np.random.default_rng(5)
+    n = 96
+    x = _laplace_mix(rng, n, 20011)
+    x[:, 3] *= tiny
+    mu = x.mean(axis=1)
+    xc = x - mu[:, None]
+    k = np.linalg.cholesky(np.linalg.inv(xc @ xc.T / x.shape[1])).T
+    d = pa.DensityType.tanh()
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    for scale in (0.1, 1.0, 30.0):
+        w = scale * (np.linalg.qr(rng.normal(size=(n, n)))[0] @ k)
+        ll, b = ctx.eval_loss_screen(w, mu, d)
+        lo, _, _ = ctx.eval_split(w, mu, d, False, need_y2=False)
+        assert np.all(np.abs(lo["ll"] - ll) <= b), (scale, np.max(np.abs(lo["ll"] - ll) / b))
+        assert np.max(b / np.abs(lo["ll"])) <= 1e-4
