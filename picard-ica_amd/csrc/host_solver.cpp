@@ -440,8 +440,14 @@ class TransformWorker {
 
 Solver::~Solver() = default;
 
-// screen / full-pass time ratio of the first-try policy (C3 on MI355X: 28 / 83 ms)
-static constexpr double kScreenCostRatio = 0.34;
+// screen / full-pass time ratio of the first-try policy, from the pass shape alone (every rank
+// computes the same value): kernel time ∝ nc²·T (MI355X, C3 = 128² × 1e8: screen 18.6 ms, fused
+// pass 84 ms) plus a fixed cost per call (≈ 0.08 / 0.10 ms: launches, copies, synchronisation).
+// C3: 0.22; C2 (64² × 1e6): 0.41.
+static double screen_cost_ratio(size_t nc, uint64_t t) {
+  const double w = (double)nc * (double)nc * (double)t / (128.0 * 128.0 * 1e8);
+  return (18.6 * w + 0.08) / (84.0 * w + 0.10);
+}
 
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first,
                                      bool first_loss_only, bool full_first) {  // core.rs:99-150
@@ -552,7 +558,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     // running estimate of p is below 1 − t_s/t_f (measured running means). p is estimated
     // per state of the previous search (accepted at try 1 or not: on C3 the first tries
     // alternate, 0.6 vs 1.0 acceptance), Laplace-smoothed over this fit's first tries.
-    // t_s/t_f: kScreenCostRatio (rank-independent; see below).
+    // t_s/t_f: screen_cost_ratio (rank-independent; see below).
     // The gradient fallback (full_first) is accepted at try 1 almost always: full pass.
     // Schedule only: no decision changes.
     bool screen = ortho && !keep_y_ && screen_ok_;
@@ -561,12 +567,12 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       if (full_first) {
         screen = false;
       } else if (first_policy) {
-        // t_s/t_f is a constant (C3: 28 / 83 ms), not the measured means: with one RCCL
+        // t_s/t_f is a model of the shape, not the measured means: with one RCCL
         // communicator every rank must take the same branch (the screen and the full
         // pass issue different all-reduces), and p_acc is built from decisions alone
         const int st = first_full_ ? 1 : 0;
         const double p_acc = (first_acc_[st] + 1.0) / (first_n_[st] + 2.0);
-        screen = p_acc < 1.0 - kScreenCostRatio;
+        screen = p_acc < 1.0 - screen_cost_ratio(n, T_);
       }
     }
     if (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
