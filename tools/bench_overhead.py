@@ -1,7 +1,7 @@
 """Fixed host-side cost of one evaluator call (upload of W and its digits, launch, the
 stats download and synchronisation) at a tiny T where the kernels take microseconds: wall
 time per call minus HIP-event kernel time. W alternates between two values so that the
-digit split is redone as in a line search. Usage: python tools/bench_overhead.py [reps]"""
+digit split is redone as in a line search. Usage: python tools/bench_overhead.py [reps] [N] [T]"""
 import os
 import sys
 import time
@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import picard_ica_amd as pa  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-n, t = 128, 65536
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+t = int(float(sys.argv[3])) if len(sys.argv) > 3 else 65536
 ctx = pa.DeviceContext(0)
 ctx.generate(n, t, 42)
 mu = ctx.rowsum() / t
