@@ -502,6 +502,20 @@ __host__ __device__ inline double finalize_row(int dens, double alpha, double n,
 // density interleave widths (register budget: fused 256 VGPRs, split kernels 128)
 constexpr int FUSED_NW = 2, LOSS_NW = 1, FROMY_NW = 1;
 
+// End-of-block barrier of the store-epilogue kernels (k_ystore, k_tiled_yw):
+// waits for this wave's LDS-DMA of the next block — issued BEFORE the block's
+// NST global stores — but not for the stores themselves. vmcnt counts loads,
+// stores and LDS-DMA together in issue order (MI355X_MICROARCH.md 's_waitcnt
+// vmcnt(N)'), and __syncthreads() drains it to 0, which put every block's
+// store round trip on the critical path. NST must be the exact number of
+// vector-memory instructions this wave issued after its DMA (0 drains all).
+template <int NST>
+__device__ __forceinline__ void dma_barrier() {
+  static_assert(NST >= 0 && NST < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 #include "ozaki.inc"  // the int8-digit Y stage (k_eval_fused<4, …, OZ> uses it too)
 
 // ---------------------------------------------------------------------------
@@ -1213,20 +1227,6 @@ constexpr int TL_KMAX = 256;  // features per phase-1 chunk (W fragments in VGPR
 
 __host__ __device__ inline size_t tl_frag(uint64_t tt, int ib, int ts, int r, int nib) {
   return ((((size_t)tt * nib + ib) * TL_TS + ts) * 4 + r) * 64;
-}
-
-// End-of-block barrier of the store-epilogue kernels (k_ystore, k_tiled_yw):
-// waits for this wave's LDS-DMA of the next block — issued BEFORE the block's
-// NST global stores — but not for the stores themselves. vmcnt counts loads,
-// stores and LDS-DMA together in issue order (MI355X_MICROARCH.md 's_waitcnt
-// vmcnt(N)'), and __syncthreads() drains it to 0, which put every block's
-// store round trip on the critical path. NST must be the exact number of
-// vector-memory instructions this wave issued after its DMA (0 drains all).
-template <int NST>
-__device__ __forceinline__ void dma_barrier() {
-  static_assert(NST >= 0 && NST < 64, "vmcnt field");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
-  __builtin_amdgcn_s_barrier();
 }
 
 // XCD-aware decode of a 1D grid into (sample range x, role): blocks b and b + 8
@@ -3582,9 +3582,35 @@ struct DeviceCtx : Evaluator {
     return true;
   }
 
+  // the non-specialised fp32 screen (k_screen_oz; PICARD_SCREEN_WS=1: the warp-specialised
+  // k_eval_loss_oz<…, F32L> instead)
+  bool screen_nows_ = std::getenv("PICARD_SCREEN_WS") == nullptr;
+  template <int DMAX, int NB>
+  void launch_screen_oz(double alpha, double* st_rows) {
+    constexpr int NCP = 16 * NB, KSO = NB == 8 ? 2 : 1, U = 16 / NB, SLOT = (DMAX + 1) * KSO * 1024;
+    const uint64_t n_blocks = (n_local_ + 15) / 16;
+    uint64_t bpw;
+    const int nwg = partition((n_blocks + U - 1) / U, &bpw);
+    bpw *= U;  // 16-sample blocks per workgroup, whole steps
+    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
+    if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
+    if (oz_kso() != KSO) throw computation_error("int8 digit image of another layout");
+    const size_t lds = (size_t)3 * U * SLOT + (size_t)3 * U * 256 + (size_t)U * NCP * 2 * sizeof(double);
+    lds_attr((const void*)k_screen_oz<DMAX, NB>, (int)lds);
+    HIP_OK(hipEventRecord(ev[1], stream));
+    k_screen_oz<DMAX, NB><<<nwg, OZW_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, alpha, bpw, n_blocks, part);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
+        part, nwg, 2 * NCP, 0, NCP, (int)kept_nc_pending, 2, st_rows, DENS_TANH, alpha, (double)n_local_, 1);
+    HIP_OK(hipGetLastError());
+    ++n_int8_passes_;
+    ++n_screen_passes_;
+  }
   template <int NB>
   void screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
-    if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);
+    if (f32l && dmax == 3 && screen_nows_) launch_screen_oz<3, NB>(d.alpha, st_rows);
+    else if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);
     else if (f32l) launch_loss_oz<DENS_TANH, false, 4, true, NB>(d.alpha, false, st_rows);
     else if (d.kind == DENS_TANH && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, false, NB>(d.alpha, false, st_rows);
     else if (d.kind == DENS_TANH) launch_loss_oz<DENS_TANH, false, 4, false, NB>(d.alpha, false, st_rows);
