@@ -174,6 +174,7 @@ def _load():
         "pc_ctx_eval": (C.c_int, [vp, d, u64, d, _Density, C.c_uint32, d, cp, sz]),
         "pc_ctx_eval_loss": (C.c_int, [vp, d, u64, d, _Density, C.c_uint32, d, P(i32), cp, sz]),
         "pc_ctx_eval_loss_multi": (C.c_int, [vp, d, d, u64, d, _Density, d, u64, d, d, cp, sz]),
+        "pc_ctx_eval_loss_multi_bound": (C.c_int, [vp, d, d, u64, d, _Density, d, u64, d, d, cp, sz]),
         "pc_ctx_eval_complete": (C.c_int, [vp, _Density, C.c_uint32, d, cp, sz]),
         "pc_ctx_rowsum": (C.c_int, [vp, d, cp, sz]),
         "pc_ctx_gram": (C.c_int, [vp, d, d, cp, sz]),
@@ -214,7 +215,7 @@ EXPORTED = [
     "pc_group_create_local", "pc_group_destroy", "pc_ctx_create_in_group", "pc_ctx_comm_stats", "pc_ctx_abort",
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
-    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
+    "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
     "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
@@ -650,6 +651,21 @@ class DeviceContext:
         _raise(lib.pc_ctx_eval_loss_multi(self.h, _ptr(w), _ptr(z), nc, _ptr(mu_a) if mu_a is not None else None,
                                           density._c(), _ptr(al), len(al), _ptr(ll), _ptr(y2), err, len(err)), err)
         return ll, y2
+
+    def eval_loss_multi_bound(self, w, z, alphas, mu=None, density: DensityType = DensityType()):
+        """pc_ctx_eval_loss_multi_bound: (Σℓ estimate, bound on its distance to the exact pass)
+        of (w + α_j·z)(X − μ) for every α_j, each [n_alpha, nc]."""
+        w, z = _c64(w), _c64(z)
+        nc = w.shape[0]
+        al = _c64(np.asarray(alphas, dtype=np.float64).ravel())
+        mu_a = _c64(mu) if mu is not None else None
+        ll = np.empty((len(al), nc))
+        bnd = np.empty((len(al), nc))
+        err = _errbuf()
+        _raise(lib.pc_ctx_eval_loss_multi_bound(self.h, _ptr(w), _ptr(z), nc,
+                                                _ptr(mu_a) if mu_a is not None else None, density._c(), _ptr(al),
+                                                len(al), _ptr(ll), _ptr(bnd), err, len(err)), err)
+        return ll, bnd
 
     def last_timing(self):
         k, c = C.c_double(), C.c_double()

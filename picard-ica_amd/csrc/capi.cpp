@@ -423,6 +423,19 @@ int pc_ctx_eval_loss_multi(pc_ctx* c, const double* w, const double* z, uint64_t
   });
 }
 
+int pc_ctx_eval_loss_multi_bound(pc_ctx* c, const double* w, const double* z, uint64_t nc, const double* mu,
+                                 pc_density d, const double* alphas, uint64_t n_alpha, double* ll_out,
+                                 double* bnd_out, char* err, size_t errlen) {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
+    if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
+    if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
+    if (n_alpha == 0) return;
+    c->ev->want_y2 = false;
+    if (!c->ev->eval_loss_multi_bound(w, z, nc, mu, d, alphas, (int)n_alpha, ll_out, bnd_out))
+      throw computation_error("bounded multi-try pass not available here");
+  });
+}
+
 int pc_ctx_eval_complete(pc_ctx* c, pc_density d, uint32_t flags, double* stats, char* err, size_t errlen) {
   return guarded_on(c->ev.get(), err, errlen, [&] {
     // only the entries [G | H | Σψ′] are written; Σℓ, Σy² of `stats` are left as they are

@@ -1837,11 +1837,16 @@ k_multi_loss2(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int 
 // LDS, and the pair evaluates the tries on y = Y + α_j·Z exactly as k_multi_loss2 does (wave
 // w takes the tries j ≡ w >> 2 mod 2). Y and Z carry fp64-GEMM accuracy (ozaki.inc); like the
 // fp64 form, Y_α = Y + α·Z agrees with a per-try pass to rounding.
-template <int KSO, int DENS, bool NEED_Q>
+// F32 (tanh, no Σy²): the tries' row terms in fp32 — y_j = fl32(fl32(Y) + α_j·fl32(Z)) and
+// loss_acc4_f32y as in the orthogonal screen — returning per try [Σℓ raw | Σ|y_j|] and per
+// row Σ|Y|, Σ|Z| (after the ML_NA tries' slots), from which DeviceCtx::eval_loss_multi_bound
+// bounds each try's distance to the exact pass at W + α_j·Z.
+template <int KSO, int DENS, bool NEED_Q, bool F32 = false>
 __global__ void __launch_bounds__(FUSED_THREADS, 2)
 k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc, const uint8_t* __restrict__ wsl_g,
                  const double* __restrict__ wsc, int ncp, double alpha, const double* __restrict__ alphas, int na,
                  uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials, uint64_t nwgx) {
+  static_assert(!F32 || (DENS == DENS_TANH && !NEED_Q), "fp32 tries: tanh without Σy²");
   constexpr int TILE = oz_block_bytes<KSO>(), NITEM = OZ_SLICES * KSO + 1, NU = (NITEM + 7) / 8;
   constexpr int SLOT = TILE + 256, KSW = KSO < 2 ? 2 : KSO;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1871,6 +1876,8 @@ k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc
   const double rsc = active ? wsc[yz * 256 + row] : 0.0;
   double aj[ML2_TRIES];
   RowAcc racc[ML2_TRIES];
+  double sabs = 0.0;  // F32: Σ|Y| (yz = 0) or Σ|Z| (yz = 1) of this lane's samples
+  const float c32 = (float)(m2a * fm::LOG2E);
 #pragma unroll
   for (int u = 0; u < ML2_TRIES; ++u) aj[u] = (yz + 2 * u < na) ? alphas[yz + 2 * u] : 0.0;
   const int my_na = na > yz ? (na - yz + 1) / 2 : 0;
@@ -1906,6 +1913,9 @@ k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc
         const d4 v = oz_combine(acc, rsc, x4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) *exch(cur, yz, r) = v[r];
+        if constexpr (F32)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sabs += fabs(v[r]);
       }
       __syncthreads();  // exchange visible; this wave's LDS-DMA of block b + 1 landed
       if (active) {
@@ -1915,25 +1925,47 @@ k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc
           yv[r] = *exch(cur, 0, r);
           zv[r] = *exch(cur, 1, r);
         }
+        if constexpr (F32) {
+          const f4 y32 = {(float)yv[0], (float)yv[1], (float)yv[2], (float)yv[3]};
+          const f4 z32 = {(float)zv[0], (float)zv[1], (float)zv[2], (float)zv[3]};
 #pragma unroll
-        for (int u = 0; u < ML2_TRIES; ++u) {
-          if (u < my_na) {
-            d4 yj;
+          for (int u = 0; u < ML2_TRIES; ++u) {
+            if (u < my_na) {
+              const float a32 = (float)aj[u];  // α_j = 2^-k: exact
+              f4 yj;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj[u], zv[r], yv[r]);
-            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, s_exp_tab, racc[u]);
-            if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
+              for (int r = 0; r < 4; ++r) yj[r] = __builtin_fabsf(__builtin_fmaf(a32, z32[r], y32[r]));
+              loss_acc4_f32y(yj, c32, racc[u]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < ML2_TRIES; ++u) {
+            if (u < my_na) {
+              d4 yj;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj[u], zv[r], yv[r]);
+              loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, s_exp_tab, racc[u]);
+              if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
+            }
           }
         }
       }
       cur ^= 1;
     }
   }
-  double* out = partials + (size_t)wx * ML_NA * 2 * ncp;
+  double* out = partials + (size_t)wx * (ML_NA * 2 + (F32 ? 2 : 0)) * ncp;
 #pragma unroll
   for (int u = 0; u < ML2_TRIES; ++u) {
     if (u < my_na) {
-      double l = acc_ll<DENS>(racc[u], inv_alpha, b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0), q = racc[u].q;
+      double l, q;
+      if constexpr (F32) {  // raw Σℓ = Σ|y| + (ln2/α)·Σ log2 Π((1 + 2^z)/2); Σ|y_j|
+        l = __builtin_fma(racc[u].g, fm::LN2 * inv_alpha, racc[u].l);
+        q = racc[u].l;
+      } else {
+        l = acc_ll<DENS>(racc[u], inv_alpha, b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0);
+        q = racc[u].q;
+      }
       l += __shfl_xor(l, 16); l += __shfl_xor(l, 32);
       q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
       if (active && lk == 0) {
@@ -1942,6 +1974,10 @@ k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc
         out[(j * 2 + 1) * ncp + row] = q;
       }
     }
+  }
+  if constexpr (F32) {
+    sabs += __shfl_xor(sabs, 16); sabs += __shfl_xor(sabs, 32);
+    if (active && lk == 0) out[(ML_NA * 2 + yz) * ncp + row] = sabs;
   }
 }
 
@@ -2924,21 +2960,23 @@ struct DeviceCtx : Evaluator {
   }
   template <int KSO, int D>
   void multi2_oz_launch(int ncp, double alpha, const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks,
-                        double* part) {
+                        double* part, bool f32 = false) {
     const int nroles = (ncp / 16 + 3) / 4;
     const size_t lds = (size_t)2 * (oz_block_bytes<KSO>() + 256) + (size_t)2 * 4 * 2 * 4 * 64 * sizeof(double);
-    auto k = want_y2 ? k_multi_loss2_oz<KSO, D, true> : k_multi_loss2_oz<KSO, D, false>;
+    auto k = f32 && D == DENS_TANH ? k_multi_loss2_oz<KSO, DENS_TANH, false, true>
+             : want_y2            ? k_multi_loss2_oz<KSO, D, true>
+                                  : k_multi_loss2_oz<KSO, D, false>;
     lds_attr((const void*)k, (int)lds);
     k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, ncp, alpha, dal, na, bpw,
                                                              n_blocks, part, (uint64_t)nwg);
   }
   template <int D>
   void multi2_oz_dispatch(int ncp, double alpha, const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks,
-                          double* part) {
+                          double* part, bool f32 = false) {
     switch (oz_kso()) {
-      case 1: multi2_oz_launch<1, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
-      case 2: multi2_oz_launch<2, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
-      default: multi2_oz_launch<4, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      case 1: multi2_oz_launch<1, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part, f32); break;
+      case 2: multi2_oz_launch<2, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part, f32); break;
+      default: multi2_oz_launch<4, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part, f32); break;
     }
   }
   template <int D>
@@ -3036,6 +3074,114 @@ struct DeviceCtx : Evaluator {
       std::memcpy(ll_out + (size_t)j * nc, h.data() + (size_t)(j * 2 + 0) * nc, nc * sizeof(double));
       std::memcpy(y2_out + (size_t)j * nc, h.data() + (size_t)(j * 2 + 1) * nc, nc * sizeof(double));
     }
+  }
+  // Non-ortho tries with fp32 row terms and a rigorous bound (Evaluator::eval_loss_multi_bound):
+  // tanh without Σy², the int8 stage at nf ≤ 256. Per try j and row i, against the exact pass
+  // at W + α_j·Z (whose y differs from Y + α_j·Z by fp64 rounding, inside the 1e-10 slack):
+  //   |ỹ − y| ≤ 2^-24·(|Y| + α_j|Z|) (the fp32 conversions) + 2^-24·|ỹ| (the fp32 fma)
+  //             + 3·2^-125 (subnormal results of the three roundings),
+  //   Σ|ỹ| in fp32 per 4 samples: ≤ 2^-23·Σ|ỹ| (1.0001 covers the higher orders), ℓ Lipschitz 1,
+  //   the log term: screen_f32_block_bound per 4 samples (the orthogonal screen's constants),
+  // so bnd = 2^-24·1.0001·(ΣY + α_jΣZ) + 2^-22·1.0001·Σ|ỹ| + (ldx/4)·block + 3·2^-125·ldx
+  //          + 1e-10·Σℓ. A rank whose scales leave the fp32 range (or that has no digit image)
+  // runs the exact kernel into the same layout with zero bound terms: every rank issues the
+  // same all-reduce, and each rank's share of the bound covers its own arithmetic.
+  // Off by default (PICARD_MULTI_F32=1 turns it on): on C4 the pass takes 31.7 ms instead of
+  // 41.2, but near convergence the tries differ by less than the fp32 bound (≈ 1e-4 in loss
+  // units), so 28 of 128 searches paid a full pass for a try the exact pass then rejected
+  // (whole fit 15.6 s against 15.0; profiles/r03_d/c4_multi_bound.txt).
+  bool multi_f32_ = std::getenv("PICARD_MULTI_F32") != nullptr;
+  bool eval_loss_multi_bound(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
+                             const double* alphas, int na, double* ll_out, double* bnd_out) override {
+    if (!multi_f32_ || !multi_loss_ok(nc, d) || d.kind != DENS_TANH || want_y2 || na > ML_NA || yw_ks(nf) == 0)
+      return false;
+    HIP_OK(hipSetDevice(device));
+    const int ncp = (int)((nc + 31) / 32 * 32);
+    std::vector<double> al(ML_NA, 0.0);
+    for (int j = 0; j < na; ++j) al[j] = alphas[j];
+    double* dal = ensure(d_w, cap_w, (size_t)ML_NA);
+    HIP_OK(hipEventRecord(ev[0], stream));
+    HIP_OK(hipMemcpyAsync(dal, al.data(), ML_NA * sizeof(double), hipMemcpyHostToDevice, stream));
+    const double* dmu = resident_mu(mu);
+    const size_t pst = (size_t)(ML_NA * 2 + 2) * ncp;
+    const uint64_t n_blocks = std::max<uint64_t>((n_local_ + 15) / 16, 1);
+    const int nroles = (ncp / 16 + 3) / 4;
+    const int nwg = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)2 * n_cu / nroles, n_blocks));
+    const uint64_t bpw = (n_blocks + nwg - 1) / nwg;
+    double* part = ensure(d_part, cap_part, (size_t)nwg * pst);
+    const size_t nst = (size_t)2 * na * nc + 3 * nc;  // [tries: Σℓ, Σ|ỹ|] [ΣY] [ΣZ] [constant bound]
+    double* st = ensure(d_stats, cap_stats, nst);
+    bool oz = y_stage_ != 1 && dmu == nullptr && ensure_xsl();
+    if (oz) upload_wsl2(w, z, nc);
+    oz = oz && xsl_valid_;
+    // fp32 range: every |Y|, |Z| scale 2^(f_i + e_t − 20) in [2^-100, 2^98]
+    bool f32 = oz && xsc_range_ok_;
+    for (int m = 0; f32 && m < 2; ++m) {
+      const double* a = m == 0 ? w : z;
+      for (size_t i = 0; f32 && i < nc; ++i) {
+        double mx = 0.0;
+        for (size_t k = 0; k < nf; ++k) mx = std::max(mx, std::fabs(a[i * nf + k]));
+        if (!(mx > 0.0)) continue;
+        int e = 0;
+        (void)std::frexp(mx, &e);
+        if (e - 20 + xsc_emin_ < -100 || e - 20 + xsc_emax_ > 98) f32 = false;
+      }
+    }
+    if (oz) {
+      HIP_OK(hipEventRecord(ev[1], stream));
+      multi2_oz_dispatch<DENS_TANH>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part, f32);
+      ++n_int8_passes_;
+    } else {  // no digit image: the fp64 multi-try pass (exact sums, zero bound terms), same layout
+      const int ks = yw_ks(nf), nfp = 4 * ks;
+      std::vector<double> wt((size_t)2 * nfp * ncp + ML_NA, 0.0);
+      for (size_t i = 0; i < nc; ++i)
+        for (size_t k = 0; k < nf; ++k) {
+          wt[k * ncp + i] = w[i * nf + k];
+          wt[(size_t)nfp * ncp + k * ncp + i] = z[i * nf + k];
+        }
+      for (int j = 0; j < na; ++j) wt[(size_t)2 * nfp * ncp + j] = alphas[j];
+      double* dw = ensure(d_w, cap_w, wt.size());
+      HIP_OK(hipMemcpyAsync(dw, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+      HIP_OK(hipEventRecord(ev[1], stream));
+      multi2_dispatch<DENS_TANH>(ks, ncp, dw, dw + (size_t)nfp * ncp, dmu, d.alpha, dw + (size_t)2 * nfp * ncp, na,
+                                 nwg, bpw, n_blocks, part);
+      HIP_OK(hipStreamSynchronize(stream));  // wt is pageable and local
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    const size_t pstu = f32 ? pst : (size_t)ML_NA * 2 * ncp;
+    k_reduce_rows<<<(2 * na * (int)nc + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pstu, 0, ncp, (int)nc, 2 * na, st,
+                                                                        DENS_TANH, d.alpha, (double)n_local_, -1);
+    HIP_OK(hipGetLastError());
+    if (f32) {
+      k_reduce_rows<<<(2 * (int)nc + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pst, (size_t)ML_NA * 2 * ncp,
+                                                                         ncp, (int)nc, 2, st + (size_t)2 * na * nc,
+                                                                         -1, 0.0, 0.0, 0);
+      HIP_OK(hipGetLastError());
+    } else {
+      HIP_OK(hipMemsetAsync(st + (size_t)2 * na * nc, 0, 2 * nc * sizeof(double), stream));
+    }
+    double* cb = (double*)pin_acquire(pin_in_, nc * sizeof(double));
+    const double cst = f32 ? (double)(ldx / 4) * screen_f32_block_bound(d.alpha) + 3.0 * 0x1p-125 * (double)ldx : 0.0;
+    for (size_t i = 0; i < nc; ++i) cb[i] = cst;
+    HIP_OK(hipMemcpyAsync(st + (size_t)2 * na * nc + 2 * nc, cb, nc * sizeof(double), hipMemcpyHostToDevice, stream));
+    pin_release(pin_in_);
+    allreduce(st, nst, "loss_multi_bound");
+    std::vector<double> h(nst);
+    const double* staged = d2h_enqueue(st, nst);
+    finish_timing(true, 3);
+    copy_out(h.data(), staged, nst);
+    const double* sy = h.data() + (size_t)2 * na * nc;
+    const double* sz = sy + nc;
+    const double* sc = sz + nc;
+    for (int j = 0; j < na; ++j)
+      for (size_t i = 0; i < nc; ++i) {
+        const double l = h[((size_t)j * 2 + 0) * nc + i], ya = h[((size_t)j * 2 + 1) * nc + i];
+        ll_out[(size_t)j * nc + i] = l;
+        bnd_out[(size_t)j * nc + i] = 0x1p-24 * 1.0001 * (sy[i] + std::fabs(alphas[j]) * sz[i]) +
+                                      0x1p-22 * 1.0001 * std::fabs(ya) + sc[i] + 1e-10 * std::fabs(l);
+      }
+    return true;
   }
   bool multi_loss_ok(size_t nc, pc_density d) const {
     return nc <= 256 && (d.kind == DENS_TANH || d.kind == DENS_EXP || d.kind == DENS_CUBE) &&

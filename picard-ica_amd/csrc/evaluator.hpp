@@ -111,6 +111,15 @@ class Evaluator {
     (void)w; (void)z; (void)nc; (void)mu; (void)d; (void)alphas; (void)na; (void)ll_out; (void)y2_out;
     return false;
   }
+  // The same tries with a rigorous bound instead of exact sums (tanh, Σy² not needed):
+  // |Σℓ_j,i − ll_out[j][i]| ≤ bnd_out[j][i] where Σℓ_j,i is what the exact pass at
+  // W + α_j·Z gives. false = not available (the caller uses eval_loss_multi); must be
+  // decided from rank-independent inputs only (every rank takes the same branch).
+  virtual bool eval_loss_multi_bound(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
+                                     const double* alphas, int na, double* ll_out, double* bnd_out) {
+    (void)w; (void)z; (void)nc; (void)mu; (void)d; (void)alphas; (void)na; (void)ll_out; (void)bnd_out;
+    return false;
+  }
   // JADE sweeps (jade.rs:37-69) on the np = n(n+1)/2 cumulant matrices A, packed
   // position-major (A[pos(k,l)·np + m], k ≤ l, pos as in jade_warm_start). On
   // success v (n×n, row-major) holds the accumulated rotation V and *log the

@@ -483,12 +483,20 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       // Non-ortho: Y_α = Y + α·Z is linear in α, so the remaining tries share
       // one pass (see eval_loss_multi); only the accepted try is evaluated in full.
       const size_t na = tries - k;
-      std::vector<double> alphas(na), ll(na * n), y2(na * n);
+      std::vector<double> alphas(na), ll(na * n), y2(na * n), bnd;
       for (size_t j = 0; j < na; ++j) alphas[j] = j == 0 ? alpha : alphas[j - 1] / 2.0;
       Mat wt = matmul(W_, P_);
       Mat zt = matmul(matmul(direction, W_), P_);
-      if (ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
-                               alphas.data(), (int)na, ll.data(), y2.data())) {
+      // without Σy² in the loss (not extended), the tries may come with a bound instead of
+      // exact sums (fp32 row terms); every decision is then taken on exact values (below)
+      bool bounded = false;
+      if (!extended_) {
+        bnd.assign(na * n, 0.0);
+        bounded = ev_->eval_loss_multi_bound(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
+                                             alphas.data(), (int)na, ll.data(), bnd.data());
+      }
+      if (bounded || ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
+                                          alphas.data(), (int)na, ll.data(), y2.data())) {
         ++last_evals_;
         ++total_evals_;
         EvalStats ls;
@@ -518,7 +526,26 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           r.tries = k + j + 1;
           bool singular;
           const double loss = loss_of(ls, r.w, signs_, &singular, dsg[j], dla[j]);
-          if (loss < current_loss_) {
+          if (bounded) {
+            // core.rs:127-140 on the exact loss: a try whose lower bound cannot beat the
+            // current loss fails; the first one that might is evaluated in full (that pass is
+            // the new iterate if it is accepted) and decided on its exact loss
+            double eb = 0.0;
+            for (size_t i = 0; i < n; ++i) eb += std::fabs(signs_[i]) * bnd[j * n + i] / (double)T_;
+            if (!singular && loss - eb < current_loss_) {
+              EvalStats full;
+              evaluate(r.w, &full);
+              const double exact = loss_of(full, r.w, signs_, &singular, dsg[j], dla[j]);
+              if (exact < current_loss_) {
+                r.stats = std::move(full);
+                r.partial = false;
+                r.loss = exact;
+                r.success = true;
+                r.step = scale(direction, a);
+                return r;
+              }
+            }
+          } else if (loss < current_loss_) {
             evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
             r.partial = false;
             r.loss = loss_of(r.stats, r.w, signs_, &singular);
