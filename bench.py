@@ -322,7 +322,7 @@ def main():
     i8 = int8_timed > 0
     kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2" + (",i8-digit Y>" if i8 else ">"), 4.0),
              "loss": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2>" if i8 else "k_eval_loss2<tanh,nostore,noY2>", 2.0),
-             "screen": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2,D<=3,fp32 l> (line-search screen)", 2.0)}
+             "screen": ("k_screen_oz", "k_screen_oz<D<=3, NB=8> (line-search screen, fp32 l)", 2.0)}
     rooflines = []
     for kind, (short, label, c) in kinds.items():
         ms, nl = brk.get(kind, (0.0, 0))

@@ -48,9 +48,10 @@ extern "C" {
 /* ABI revision of this header. 2: pc_host_evaluator grew the eval_loss_multi and
  * eval_loss_screen slots (a caller built against revision 1 must be rebuilt), the
  * rank-group entry points (pc_group_*, pc_ctx_create_in_group, pc_ctx_comm_stats,
- * pc_ctx_abort) and pc_ctx_release_caches were added. pc_abi_version() returns the
- * revision the library was built with. */
-#define PC_ABI_VERSION 2
+ * pc_ctx_abort) and pc_ctx_release_caches were added. 3: pc_ctx_eval_loss_multi_bound
+ * was added (no layout change). pc_abi_version() returns the revision the library was
+ * built with. */
+#define PC_ABI_VERSION 3
 
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {

@@ -11,7 +11,8 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_eval_fused": lambda n, t: 8.0 * n * t, "k_eval_loss": lambda n, t: 8.0 * n * t}
+KERNELS = {"k_eval_fused": lambda n, t: 8.0 * n * t, "k_eval_loss": lambda n, t: 8.0 * n * t,
+           "k_screen_oz": lambda n, t: 8.0 * n * t}
 
 
 def main():
@@ -25,7 +26,7 @@ def main():
                     # the solver's instantiations: tanh, no H (and no Σy²); the fused pass at
                     # 64 < nc <= 128 is the warp-specialised k_eval_fused_ws<dens, Q>
                     tmpl = name.split("<")[1] if "<" in name else ""
-                    if short in name and (tmpl.startswith("8, ") or
+                    if short in name and (tmpl.startswith("8, ") or (short == "k_screen_oz" and "<3, 8>" in name) or
                                           (short == "k_eval_fused" and "k_eval_fused_ws<0," in name) or
                                           (short == "k_eval_loss" and ("k_eval_loss2<0, false," in name or
                                                                        "k_eval_loss_oz<0, false," in name))):
