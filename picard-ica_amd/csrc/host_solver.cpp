@@ -468,7 +468,14 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
         map1_ms_ = now_ms() - tm;
         if (tries > 1) {
-          if (!ahead_) ahead_.reset(new TransformWorker());
+          if (!ahead_) {
+            ahead_.reset(new TransformWorker());
+            // the helper keeps a core of its own: this thread's OpenMP team gives one up. A
+            // stale helper map (a search that ended early) otherwise shares a core with a team
+            // thread, and every barrier of the team's N³ products waits for that thread (one
+            // rank of C3/8: a fallback's try-1 Taylor series took 9.4 ms instead of 0.2)
+            omp_set_num_threads(std::max(1, omp_get_max_threads() - 1));
+          }
           ahead_->submit(direction, W_, tries);
         }
       } else {
