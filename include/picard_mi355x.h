@@ -132,7 +132,8 @@ typedef struct pc_ctx pc_ctx;
 
 /* RCCL bootstrap for one-process-per-GPU runs: rank 0 calls pc_rccl_unique_id,
  * the 128-byte id is broadcast by the caller (e.g. torch.distributed), every
- * rank then creates its context with it. world_size == 1 needs no id. */
+ * rank then creates its context with it. world_size == 1 needs no id; given one,
+ * the context is a one-rank RCCL communicator (the RCCL code path on one GPU). */
 int pc_rccl_unique_id(char id_out[128]);
 
 /* Each rank owns the samples [t0, t0 + n_local) of a global matrix with

@@ -522,8 +522,9 @@ class LocalGroup:
 class DeviceContext:
     """pc_ctx: one GPU, one contiguous T shard of X resident in HBM. With `group`
     (a LocalGroup) the context is rank `rank` of that in-process group; with
-    world_size > 1 and an `rccl_id` it is one rank of an RCCL communicator; with
-    world_size > 1 and neither, a detached shard (partial sums)."""
+    an `rccl_id` it is one rank of an RCCL communicator (world_size 1 included: a
+    one-rank communicator); with world_size > 1 and neither, a detached shard
+    (partial sums)."""
 
     def __init__(self, device: int = 0, rank: int = 0, world_size: int = 1, rccl_id: Optional[bytes] = None,
                  group: Optional[LocalGroup] = None):

@@ -2521,8 +2521,16 @@ struct DeviceCtx : Evaluator {
   // Pinned host staging for the per-pass uploads (W image, W digit image): the copy is
   // issued asynchronously and an event after it guards the slot — the next writer of the
   // slot waits on that event, so no stream synchronisation follows the upload.
-  struct PinSlot { void* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; };
+  struct PinSlot { void* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; bool pending = false; unsigned flags = 0; };
   PinSlot pin_w_, pin_wsl_, pin_out_, pin_in_;
+  // Without a collective the last kernel of a pass (the fixed-order reduction) stores the
+  // statistics straight into coherent pinned host memory: no D2H copy on the call's GPU
+  // timeline. With one, the statistics stay in HBM for the all-reduce.
+  PinSlot pin_direct_{nullptr, 0, nullptr, false, hipHostMallocCoherent};
+  double* direct_acquire(size_t n) {
+    if (coll_) return nullptr;
+    return (double*)pin_acquire(pin_direct_, std::max<size_t>(n, 1) * sizeof(double));
+  }
   // D2H of n doubles through the pinned out slot (a DMA copy; a pageable destination takes a
   // staging blit and a blocking copy): enqueue now, copy_out() after the stream has synced
   const double* d2h_enqueue(const double* dsrc, size_t n) {
@@ -2541,7 +2549,7 @@ struct DeviceCtx : Evaluator {
       if (sl.p) HIP_OK(hipHostFree(sl.p));
       sl.p = nullptr;
       sl.cap = 0;
-      HIP_OK(hipHostMalloc(&sl.p, bytes, 0));
+      HIP_OK(hipHostMalloc(&sl.p, bytes, sl.flags));
       sl.cap = bytes;
     }
     if (!sl.ev) HIP_OK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
@@ -2562,8 +2570,9 @@ struct DeviceCtx : Evaluator {
     n_cu = prop.multiProcessorCount;
     // world > 1 without an RCCL id or a group: a detached shard (no communicator; every
     // statistic is this shard's partial sum and the caller adds them up)
+    // (an id at world 1: a one-rank RCCL communicator — the RCCL path on one GPU)
     if (grp) coll_ = make_local_collective(std::move(grp), rank);
-    else if (world > 1 && uid) coll_ = make_rccl_collective(rank, world, uid);
+    else if (uid) coll_ = make_rccl_collective(rank, world, uid);
     if (const char* e = std::getenv("PICARD_TEST_PIN_DIGITS")) pin_test_ = std::atoi(e) != 0;
   }
   ~DeviceCtx() override {
@@ -2571,10 +2580,10 @@ struct DeviceCtx : Evaluator {
     coll_.reset();
     for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src})
       if (p) (void)hipFree(p);
-    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsl, (void*)d_wsc})
+    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc})  // d_wsl lies inside d_wsc's allocation
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
-    for (PinSlot* sl : {&pin_w_, &pin_wsl_, &pin_out_, &pin_in_}) {
+    for (PinSlot* sl : {&pin_w_, &pin_wsl_, &pin_out_, &pin_in_, &pin_direct_}) {
       if (sl->pending) (void)hipEventSynchronize(sl->ev);
       if (sl->p) (void)hipHostFree(sl->p);
       if (sl->ev) (void)hipEventDestroy(sl->ev);
@@ -2896,6 +2905,8 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     const size_t total = EvalStats::size(nc, need_h);
     double* st = ensure(d_stats, cap_stats, total);
+    double* direct = direct_acquire(total);
+    if (direct) st = direct;
     HIP_OK(hipEventRecord(ev[0], stream));
     const int nb = pick_nb(nc);
     const int nfp = 16 * std::max(nb, 1);  // fused pass: K padded to 16·NB (host builds Wp accordingly)
@@ -2931,8 +2942,13 @@ struct DeviceCtx : Evaluator {
     } else {
       throw computation_error("no evaluation path for density id " + std::to_string(dens));
     }
-    allreduce(st, total, need_h ? "eval+H" : "eval");
-    const double* staged = d2h_enqueue(st, total);
+    const double* staged = direct;
+    if (direct) {
+      pin_release(pin_direct_);
+    } else {
+      allreduce(st, total, need_h ? "eval+H" : "eval");
+      staged = d2h_enqueue(st, total);
+    }
     HIP_OK(hipEventRecord(ev[3], stream));
     sync();
     copy_out(stats_host, staged, total);
@@ -3485,10 +3501,13 @@ struct DeviceCtx : Evaluator {
   std::vector<double> wsl_w_;
   size_t wsl_nc_ = 0;
   static constexpr size_t WSL_IMG_MAX = (size_t)32 * OZ_SLICES * 4 * 64 * 16;  // 32 row blocks × 4 k-steps
+  // one allocation [512 row scales | slice image], the layout of the pinned slot, so that one
+  // copy uploads both (a call's GPU timeline pays a dependency gap per copy)
+  static constexpr size_t WSC_BYTES = 512 * sizeof(double);
   void alloc_wsl() {
-    if (!d_wsl) {
-      HIP_OK(hipMalloc(&d_wsl, WSL_IMG_MAX));
-      HIP_OK(hipMalloc(&d_wsc, 512 * sizeof(double)));
+    if (!d_wsc) {
+      HIP_OK(hipMalloc(&d_wsc, WSC_BYTES + WSL_IMG_MAX));
+      d_wsl = (uint8_t*)d_wsc + WSC_BYTES;
     }
   }
   // the multi-try pass: W in row blocks 0–15 (scales 0–255), Z = D·W in 16–31 (256–511)
@@ -3497,15 +3516,14 @@ struct DeviceCtx : Evaluator {
     if (nc > 256) throw computation_error("int8 W image: nc > 256");
     const int ksw = wsl_ksw();
     const size_t half = (size_t)16 * OZ_SLICES * ksw * 64 * 16;
-    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, WSL_IMG_MAX + 512 * sizeof(double));
-    double* sc = (double*)(img + WSL_IMG_MAX);
+    double* sc = (double*)pin_acquire(pin_wsl_, WSC_BYTES + WSL_IMG_MAX);
+    uint8_t* img = (uint8_t*)sc + WSC_BYTES;
     std::memset(img, 0, 2 * half);
     for (int i = 0; i < 512; ++i) sc[i] = 0x1p-12;
     oz_split_rows(w, nc, nf, img, sc, ksw);
     oz_split_rows(z, nc, nf, img + half, sc + 256, ksw);
     wsl_nc_ = 0;  // the image no longer holds a single W
-    HIP_OK(hipMemcpyAsync(d_wsl, img, 2 * half, hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(d_wsc, sc, 512 * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + 2 * half, hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);
   }
   void upload_wsl(const double* w, size_t nc) {
@@ -3518,15 +3536,14 @@ struct DeviceCtx : Evaluator {
     const size_t img_bytes = (size_t)((nc + 15) / 16) * OZ_SLICES * ksw * 64 * 16;
     alloc_wsl();
     if (nc > 256) throw computation_error("int8 W image: nc > 256");
-    uint8_t* img = (uint8_t*)pin_acquire(pin_wsl_, IMG_MAX + 512 * sizeof(double));
-    double* sc = (double*)(img + IMG_MAX);
+    double* sc = (double*)pin_acquire(pin_wsl_, WSC_BYTES + IMG_MAX);
+    uint8_t* img = (uint8_t*)sc + WSC_BYTES;
     std::memset(img, 0, img_bytes);
     for (int i = 0; i < 256; ++i) sc[i] = 0x1p-12;
     oz_split_rows(w, nc, nf, img, sc, ksw);  // host_linalg.cpp: rows split over the host threads
     wsl_w_.assign(w, w + nc * nf);
     wsl_nc_ = nc;
-    HIP_OK(hipMemcpyAsync(d_wsl, img, img_bytes, hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(d_wsc, sc, 256 * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + img_bytes, hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
   // NB = 8 (64 < nc ≤ 128) or NB = 4 (32 < nc ≤ 64, nf ≤ 64; partition in 32-sample blocks,
@@ -3654,6 +3671,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     const double* dmu = resident_mu(mu);
     double* st_rows = ensure(d_stats, cap_stats, 3 * nc);  // [Σℓ | Σ|ỹ| (fp32 screen) | bound]
+    double* direct = nullptr;
     {  // the pass buffers before the image is relied on (an allocation may release it)
       uint64_t bpw0;
       const int nwg0 = partition(nb4 ? (n_local_ + 31) / 32 : (n_local_ + 15) / 16, &bpw0);
@@ -3686,6 +3704,8 @@ struct DeviceCtx : Evaluator {
     for (size_t i = 0; f32l && i < nc; ++i)
       if (!zero_row[i] && (fexp[i] - 20 + xsc_emin_ < -100 || fexp[i] - 20 + xsc_emax_ > 99)) f32l = false;
     HIP_OK(hipEventRecord(ev[0], stream));
+    direct = direct_acquire(3 * nc);  // (after the image checks: no early return holds the slot)
+    if (direct) st_rows = direct;
     if (nb4) screen_launch<4>(d, dmax, f32l, st_rows);
     else screen_launch<8>(d, dmax, f32l, st_rows);
     // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
@@ -3703,17 +3723,23 @@ struct DeviceCtx : Evaluator {
     if (f32l) bsum += std::ldexp(256.0 * pm(2) + pm(3) + pm(4) / 256.0, -46) * (1.0 + 1e-6);
     const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
     const double tail = (double)nf * bsum * xsc_sum_ * lip;
-    double* bnd = (double*)pin_acquire(pin_in_, nc * sizeof(double));  // H2D by DMA
+    // this rank's bound: summed over ranks with the statistics (its own row of the all-reduce)
+    double* bnd = direct ? direct + 2 * nc : (double*)pin_acquire(pin_in_, nc * sizeof(double));  // H2D by DMA
     for (size_t i = 0; i < nc; ++i) {
       bnd[i] = std::ldexp(tail, fexp[i] - 12) * (1.0 + 1e-12);
       // fp32 ℓ: 4 lane-blocks of 4 samples per 16-sample block of this row (padding included)
       if (f32l) bnd[i] += (double)(ldx / 4) * screen_f32_block_bound(d.alpha);
     }
-    HIP_OK(hipMemcpyAsync(st_rows + 2 * nc, bnd, nc * sizeof(double), hipMemcpyHostToDevice, stream));
-    pin_release(pin_in_);
-    allreduce(st_rows, 3 * nc, "screen");
     std::vector<double> tmp(3 * nc);
-    const double* staged = d2h_enqueue(st_rows, 3 * nc);
+    const double* staged = direct;
+    if (direct) {
+      pin_release(pin_direct_);  // the kernel writes rows 0–1, the host row 2 (disjoint)
+    } else {
+      HIP_OK(hipMemcpyAsync(st_rows + 2 * nc, bnd, nc * sizeof(double), hipMemcpyHostToDevice, stream));
+      pin_release(pin_in_);
+      allreduce(st_rows, 3 * nc, "screen");
+      staged = d2h_enqueue(st_rows, 3 * nc);
+    }
     finish_timing(true, 4);
     copy_out(tmp.data(), staged, 3 * nc);
     // the rounding slack: Σ_t |ℓ| ≤ |Σℓ| for tanh (ℓ ≥ 0), ≤ n/α for exp (|ℓ| ≤ 1/α);
