@@ -92,7 +92,28 @@ void regularize_hessian(Mat& h, const std::vector<double>& h_off, double lambda_
 }
 
 // ------------------------------------------------------------- Solver
+// Host team of the driving thread: the N×N work (Taylor series, log-determinants, L-BFGS, the
+// digit split of W) gains nothing past a few threads at N ≤ 256, and a team as wide as the
+// process's CPU share leaves no core for the line-search helper and the HIP runtime threads:
+// on a 16-CPU box the one-rank-of-8 C3 shard measured host time per iteration mean 1.4-2.0 ms,
+// p90 3-5 ms with 16 threads against 0.84-0.88 / 1.1-1.2 ms with 8 (profiles/r03_h). With 8
+// ranks per node, 8 teams as wide as the node would oversubscribe it 8×. Default
+// min(OMP max threads, 8); PICARD_HOST_THREADS overrides the cap. Read once, before any
+// omp_set_num_threads of this library.
+static int host_team_threads() {
+  static const int v = [] {
+    int cap = 8;
+    if (const char* e = std::getenv("PICARD_HOST_THREADS")) {
+      const int c = std::atoi(e);
+      if (c > 0) cap = c;
+    }
+    return std::max(1, std::min(omp_get_max_threads(), cap));
+  }();
+  return v;
+}
+
 Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
+  omp_set_num_threads(host_team_threads());
   // config.rs:104-142
   if (cfg.max_iter == 0) throw invalid_config("max_iter", "must be greater than 0");
   if (!(cfg.tol > 0.0)) throw invalid_config("tol", "must be positive");
@@ -474,7 +495,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
             // stale helper map (a search that ended early) otherwise shares a core with a team
             // thread, and every barrier of the team's N³ products waits for that thread (one
             // rank of C3/8: a fallback's try-1 Taylor series took 9.4 ms instead of 0.2)
-            omp_set_num_threads(std::max(1, omp_get_max_threads() - 1));
+            omp_set_num_threads(std::max(1, host_team_threads() - 1));
           }
           ahead_->submit(direction, W_, tries);
         }

@@ -1,4 +1,4 @@
-# usage: bash tools/gpu_hostspikes.sh TAG — the one-rank-of-8 proxy (bench.py --t 1.25e7, C3 only)
+# usage: bash tools/gpu_hostspikes.sh TAG [all] — the one-rank-of-8 proxy (bench.py --t 1.25e7, C3 only)
 # three times each under three OpenMP settings, with the per-iteration trace: host-time spikes
 TAG=$1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
@@ -14,4 +14,8 @@ run() {  # name, env...
   done
 }
 echo "nproc $(nproc) OMP_NUM_THREADS=$OMP_NUM_THREADS"
-run default OMP_DUMMY=1 && run passive OMP_WAIT_POLICY=passive && run omp8 OMP_NUM_THREADS=8
+if [ "$2" = all ]; then
+  run default OMP_DUMMY=1 && run passive OMP_WAIT_POLICY=passive && run omp8 OMP_NUM_THREADS=8
+else
+  run default OMP_DUMMY=1
+fi
