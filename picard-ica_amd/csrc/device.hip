@@ -2835,6 +2835,15 @@ struct DeviceCtx : Evaluator {
 
   static int pick_nb(size_t nc) { return nc <= 16 ? 1 : nc <= 32 ? 2 : nc <= 64 ? 4 : nc <= 128 ? 8 : 0; }
 
+  // the padded fp64 W staged in pin_w_ by run_eval, not yet copied to d_w
+  const double* wp_pending_ = nullptr;
+  size_t wp_n_ = 0;
+  void flush_wp() {
+    if (!wp_pending_) return;
+    HIP_OK(hipMemcpyAsync(d_w, wp_pending_, wp_n_ * sizeof(double), hipMemcpyHostToDevice, stream));
+    wp_pending_ = nullptr;
+  }
+
   template <int NB, bool H, int D, bool Q>
   void launch_fused(int nfp, const double* dmu, double alpha, double* st, size_t nc) {
     using S = FusedShape<NB>;
@@ -2857,6 +2866,9 @@ struct DeviceCtx : Evaluator {
     const bool oz4 = OZ4 && oz_ok && oz_kso() == 1;
     // … and its warp-specialised form on the centred resident X (PICARD_NO_WS4=1: the 8-wave kernel)
     const bool ws4 = NB == 4 && !H && dmu == nullptr && nf <= 64 && !no_ws4_;
+    // the digit-stage forms of the warp-specialised kernels never read the fp64 W: its copy is
+    // left out of the call's timeline
+    if (!((ws && oz) || (!ws && ws4 && oz4))) flush_wp();
     auto kws = oz ? k_eval_fused_ws<D, Q, true> : k_eval_fused_ws<D, Q, false>;
     auto kfu = oz4 ? k_eval_fused<NB, H, D, Q, OZ4> : k_eval_fused<NB, H, D, Q, false>;
     auto kw4 = oz4 ? k_eval_fused_ws4<D, Q, OZ4> : k_eval_fused_ws4<D, Q, false>;
@@ -2926,19 +2938,26 @@ struct DeviceCtx : Evaluator {
       std::fill(wp, wp + nwp, 0.0);
       for (size_t i = 0; i < nc; ++i)
         for (size_t k = 0; k < nf; ++k) wp[i * nfp + k] = w[i * nf + k];
-      HIP_OK(hipMemcpyAsync(d_w, wp, nwp * sizeof(double), hipMemcpyHostToDevice, stream));
-      pin_release(pin_w_);
+      wp_pending_ = wp;  // copied by launch_fused when the kernel it picks reads it
+      wp_n_ = nwp;
       oz_fused_ready_ = false;
       if (dmu == nullptr && !need_h && dens != DENS_LINEAR && oz_any(nc) && ensure_xsl()) {
         upload_wsl(w, nc);
         oz_fused_ready_ = true;
       }
-      switch (nb) {
-        case 1: dispatch_h<1>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
-        case 2: dispatch_h<2>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
-        case 4: dispatch_h<4>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
-        default: dispatch_h<8>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+      try {
+        switch (nb) {
+          case 1: dispatch_h<1>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+          case 2: dispatch_h<2>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+          case 4: dispatch_h<4>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+          default: dispatch_h<8>(need_h, want_y2, dens, nfp, dmu, alpha, st, nc); break;
+        }
+      } catch (...) {
+        wp_pending_ = nullptr;
+        throw;
       }
+      wp_pending_ = nullptr;
+      pin_release(pin_w_);  // (after the copy, if one was enqueued)
     } else {
       throw computation_error("no evaluation path for density id " + std::to_string(dens));
     }
