@@ -2425,6 +2425,25 @@ __device__ __forceinline__ double laplace_of(uint64_t st) {
 
 #include "jade_sweeps.inc"
 
+// Cumulant matrices for the sweeps from the lexicographic fourth moments M (np × np, pair
+// index m ↔ (i, j), i ≤ j, the order of jade_warm_start's pidx and pos): A[pos(k,l)][m] =
+// (q(k,l) + q(l,k)) / 2 with q = M[m][pos]/t − δ_ij δ_kl − δ_ik δ_jl − δ_il δ_jk — the host
+// build's expressions in its order (jade.rs:101-126), so the same bits.
+__global__ void __launch_bounds__(256) k_jade_cumulants(const double* __restrict__ M, const int* __restrict__ pi,
+                                                       const int* __restrict__ pj, int np, double t,
+                                                       double* __restrict__ A) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (size_t)np * np) return;
+  const int ps = (int)(e / np), m = (int)(e % np);
+  const int i = pi[m], j = pj[m], k = pi[ps], l = pj[ps];
+  const double x = M[(size_t)m * np + ps] / t;
+  const double d1 = (i == j && k == l) ? 1.0 : 0.0;
+  const double d2 = (i == k && j == l) ? 1.0 : 0.0, d3 = (i == l && j == k) ? 1.0 : 0.0;
+  const double qkl = x - d1 - d2 - d3;  // q(k, l)
+  const double qlk = x - d1 - d3 - d2;  // q(l, k): δ_ik δ_jl and δ_il δ_jk trade places
+  A[e] = (qkl + qlk) / 2.0;
+}
+
 // ---------------------------------------------------------------------------
 // Exhaustive accuracy of the fp32 transcendental instructions the line-search
 // screen uses (v_exp_f32 = 2^x, v_log_f32 = log2 x), over every fp32 input of the
@@ -2678,6 +2697,7 @@ struct DeviceCtx : Evaluator {
     ystore_upload(A.data(), nf, nf);
     const Affine jt = lcg_jump(n_tot);  // row i → i+1 at fixed t
     const uint64_t CH = 1ull << 22;
+    m4_full_ = nullptr;  // d_chunk is reused
     double* S = ensure(d_chunk, cap_chunk, nf * CH);
     for (uint64_t c0 = 0; c0 < nl; c0 += CH) {
       const uint64_t cn = std::min<uint64_t>(CH, nl - c0);
@@ -4052,6 +4072,7 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipSetDevice(device));
     resident_mu(mu);  // X is centred in place: Y = W·X
     const uint64_t CH = 1ull << 20;
+    m4_full_ = nullptr;  // d_chunk is reused
     double* Y = ensure(d_chunk, cap_chunk, nc * CH);  // first: a failed allocation releases the image
     const bool oz = ystore_oz_ok(nc);
     if (oz) upload_wsl(w, nc);
@@ -4095,6 +4116,20 @@ struct DeviceCtx : Evaluator {
   // they fit (n ≲ 66 on MI355X: np·npos·8 B over 256 CUs) and the device can
   // co-schedule the grid; otherwise the host runs the sweeps.
   bool jade_sweeps(const double* A, size_t n, size_t max_iter, double tol, double* v_out, JadeSweepLog* log) override {
+    return jade_sweeps_impl(A, n, 0.0, max_iter, tol, v_out, log);
+  }
+  // the cumulant matrices from the M the last moments4 call left in d_chunk (m4_full_)
+  bool jade_sweeps_moments(size_t n, double t, size_t max_iter, double tol, double* v_out,
+                           JadeSweepLog* log) override {
+    if (!m4_full_ || m4_nc_ != n) return false;
+    return jade_sweeps_impl(nullptr, n, t, max_iter, tol, v_out, log);
+  }
+  // M of the last moments4 call, its pair lists (inside d_chunk; cleared by every other user)
+  const double* m4_full_ = nullptr;
+  const int *m4_pi_ = nullptr, *m4_pj_ = nullptr;
+  size_t m4_nc_ = 0;
+  bool jade_sweeps_impl(const double* A, size_t n, double t, size_t max_iter, double tol, double* v_out,
+                        JadeSweepLog* log) {
     HIP_OK(hipSetDevice(device));
     if (n < 2 || n > 256) return false;
     const size_t np = n * (n + 1) / 2, npos = np;
@@ -4104,14 +4139,18 @@ struct DeviceCtx : Evaluator {
     const size_t mw = (np + JS_MAX_WG - 1) / JS_MAX_WG;
     const size_t G = (np + mw - 1) / mw;
     const size_t lds = (npos * mw + 4) * sizeof(double);
-    if (lds > 160 * 1024 || G > (size_t)n_cu || G > (size_t)JS_MAX_WG || (n - 2) * mw > (size_t)JS_ROT_MAX * JS_THREADS)
+    if (lds > 160 * 1024 || G > (size_t)n_cu || G > (size_t)JS_MAX_WG || (n - 2) * mw > (size_t)JS_ROT_ELEMS)
       return false;
     int coop = 0;
     HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
     if (!coop) return false;
-    lds_attr((const void*)k_jade_sweeps, (int)lds);
+    // four waves per workgroup (default) or one (PICARD_JADE_THREADS=64): the same arithmetic
+    const char* jt = std::getenv("PICARD_JADE_THREADS");
+    const int th = jt && std::atoi(jt) == 64 ? 64 : JS_THREADS;
+    const void* kern = th == 64 ? (const void*)k_jade_sweeps<64> : (const void*)k_jade_sweeps<JS_THREADS>;
+    lds_attr(kern, (int)lds);
     int per_cu = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_jade_sweeps, JS_THREADS, lds));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, th, lds));
     if ((size_t)per_cu * n_cu < G) return false;
     // A [npos][np] as the host built it; workgroup g loads matrices g·mw … g·mw + mw − 1
     std::vector<double> eye(n * n, 0.0);
@@ -4131,13 +4170,17 @@ struct DeviceCtx : Evaluator {
     if (const char* e = std::getenv("PICARD_JADE_BAR_BASE")) seq0 = std::strtoull(e, nullptr, 0);
     long long max_pairs = (long long)std::min<size_t>(jade_max_pairs(), (size_t)LLONG_MAX);
     HIP_OK(hipMemsetAsync(d_g, 0, 2 * G * 3 * 2 * sizeof(double), stream));  // tags 0 ≠ any seq ≥ seq0 + 1
-    HIP_OK(hipMemcpyAsync(d_a, A, npos * np * sizeof(double), hipMemcpyHostToDevice, stream));
+    if (A) {
+      HIP_OK(hipMemcpyAsync(d_a, A, npos * np * sizeof(double), hipMemcpyHostToDevice, stream));
+    } else {
+      k_jade_cumulants<<<(unsigned)((np * np + 255) / 256), 256, 0, stream>>>(m4_full_, m4_pi_, m4_pj_, (int)np, t, d_a);
+      HIP_OK(hipGetLastError());
+    }
     HIP_OK(hipMemcpyAsync(d_v, eye.data(), n * n * sizeof(double), hipMemcpyHostToDevice, stream));
     int np_i = (int)np, n_i = (int)n, npos_i = (int)npos, mw_i = (int)mw, it_i = (int)std::min<size_t>(max_iter, 1u << 30);
     double tol_d = tol;
     void* args[] = {&d_a, &np_i, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_sw, &d_th, (void*)&theta_cap, &seq0, &max_pairs};
-    HIP_OK(hipLaunchCooperativeKernel((const void*)k_jade_sweeps, dim3((unsigned)G), dim3(JS_THREADS), args,
-                                      (unsigned)lds, stream));
+    HIP_OK(hipLaunchCooperativeKernel(kern, dim3((unsigned)G), dim3((unsigned)th), args, (unsigned)lds, stream));
     int sw[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(v_out, d_v, n * n * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipMemcpyAsync(sw, d_sw, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -4202,6 +4245,7 @@ struct DeviceCtx : Evaluator {
     auto dsz = [](size_t bytes) { return (bytes + sizeof(double) - 1) / sizeof(double); };
     const size_t ints = dsz((6 * (size_t)np + packs.size()) * sizeof(int) + pmask.size());
     const size_t need = nc * CH + (mfma_path ? 2 : 1) * (size_t)np * np + ints + (mfma_path ? nsplit * slab_stride : 0);
+    m4_full_ = nullptr;
     double* Y = ensure(d_chunk, cap_chunk, need);
     double* acc = Y + nc * CH;
     double* full = mfma_path ? acc + (size_t)np * np : acc;  // the lexicographic M (fill target)
@@ -4257,6 +4301,12 @@ struct DeviceCtx : Evaluator {
     }
     HIP_OK(hipMemcpyAsync(out, full, (size_t)np * np * sizeof(double), hipMemcpyDeviceToHost, stream));
     sync();
+    if (mfma_path) {  // the lexicographic M stays for jade_sweeps_moments (the VALU path fills one triangle)
+      m4_full_ = full;
+      m4_pi_ = dpi;
+      m4_pj_ = dpj;
+      m4_nc_ = nc;
+    }
     if (!mfma_path)
       for (int p = 0; p < np; ++p)  // mirror the upper tiles
         for (int q = 0; q < p; ++q) out[(size_t)p * np + q] = out[(size_t)q * np + p];

@@ -130,6 +130,13 @@ class Evaluator {
     (void)A; (void)n; (void)max_iter; (void)tol; (void)v; (void)log;
     return false;
   }
+  // The same sweeps on the cumulant matrices of the LAST moments4 call (Q_ij = M/t − δ-terms,
+  // jade.rs:101-126, the values jade_warm_start builds on the host), formed where that call
+  // left M; false = not available (the caller builds A and calls jade_sweeps).
+  virtual bool jade_sweeps_moments(size_t n, double t, size_t max_iter, double tol, double* v, JadeSweepLog* log) {
+    (void)n; (void)t; (void)max_iter; (void)tol; (void)v; (void)log;
+    return false;
+  }
   // eval_complete into a raw packed stats buffer (C ABI)
   virtual void eval_complete_into(pc_density d, bool need_h, double* stats) {
     (void)d; (void)need_h; (void)stats;

@@ -949,6 +949,31 @@ Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, 
   const auto tj0 = std::chrono::steady_clock::now();
   ev->moments4(base.data(), n, mu, m4.data());
   const auto tj1 = std::chrono::steady_clock::now();
+  info->moments_s = std::chrono::duration<double>(tj1 - tj0).count();
+  auto device_done = [&](const JadeSweepLog& log, const Mat& v) {
+    if (verbose) {  // jade.rs:57-66
+      for (size_t k = 0; k < log.theta10.size(); ++k)
+        std::printf("JADE iteration %zu: max angle = %s\n", 10 * (k + 1), rust_e4(log.theta10[k]).c_str());
+      if (log.converged) std::printf("JADE converged after %zu iterations\n", log.sweeps);
+    }
+    info->sweeps = log.sweeps;
+    info->converged = log.converged;
+    info->on_device = true;
+    info->sweeps_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tj1).count();
+    Mat w;
+    if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
+    return w;
+  };
+  // The device sweeps on cumulant matrices formed on the device from its copy of M (the same
+  // values as the host build below): no host build, no upload
+  if (where == JADE_SWEEPS_DEVICE || where == JADE_SWEEPS_AUTO_DEVICE) {
+    JadeSweepLog log;
+    Mat v = Mat::eye(n);
+    if (ev->jade_sweeps_moments(n, T, max_iter, tol, v.data(), &log)) {
+      if (verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
+      return device_done(log, v);
+    }
+  }
   std::vector<size_t> pidx(n * n);
   {
     size_t q = 0;
@@ -988,25 +1013,11 @@ Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, 
   }
   if (verbose) std::printf("JADE: %zu cumulant matrices computed\n", np);
   Mat v = Mat::eye(n);
-  info->moments_s = std::chrono::duration<double>(tj1 - tj0).count();
   // The sweeps as one cooperative device launch (DeviceCtx::jade_sweeps) where
   // asked for and supported; the host sweeps otherwise.
   if (where == JADE_SWEEPS_DEVICE || where == JADE_SWEEPS_AUTO_DEVICE) {
     JadeSweepLog log;
-    if (ev->jade_sweeps(A.data(), n, max_iter, tol, v.data(), &log)) {
-      if (verbose) {  // jade.rs:57-66
-        for (size_t k = 0; k < log.theta10.size(); ++k)
-          std::printf("JADE iteration %zu: max angle = %s\n", 10 * (k + 1), rust_e4(log.theta10[k]).c_str());
-        if (log.converged) std::printf("JADE converged after %zu iterations\n", log.sweeps);
-      }
-      info->sweeps = log.sweeps;
-      info->converged = log.converged;
-      info->on_device = true;
-      info->sweeps_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tj1).count();
-      Mat w;
-      if (!sym_decorrelation(v, &w)) throw singular_matrix();  // jade.rs:69
-      return w;
-    }
+    if (ev->jade_sweeps(A.data(), n, max_iter, tol, v.data(), &log)) return device_done(log, v);
     if (where == JADE_SWEEPS_DEVICE) throw computation_error("device JADE sweeps not supported for this shape");
   }
   // Sweeps in the reference's cyclic (p, q) order. The np matrices are split
