@@ -144,10 +144,15 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
                  "Warning: Using a density other than tanh with extended=true and ortho=false "
                  "may result in incorrect estimation or numerical overflow\n");
   const double pf = (double)p;
+  // setup phases for PICARD_TRACE (ms since the constructor started)
+  const auto ts0 = std::chrono::steady_clock::now();
+  double tsm[5] = {0, 0, 0, 0, 0};  // rowsum, Gram, eigh, w_init + warm start, initial pass
+  auto lap = [&](int i) { tsm[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count(); };
   // center: whitening.rs:24-35 (μ folded into every pass; X is never copied)
   if (cfg.centering) {
     mu_.assign(n, 0.0);
     ev->rowsum(mu_.data());
+    lap(0);
     for (double& v : mu_) v /= pf;
     has_mu_ = true;
   }
@@ -160,10 +165,12 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
     }
     gram_ = Mat(n, n);
     ev->gram(mu, gram_.data());
+    lap(1);
     has_gram_ = true;
     std::vector<double> lam;
     Mat u;
     eigh(gram_, &lam, &u);
+    lap(2);
     // descending singular values s_i = sqrt(λ), columns of U in that order
     std::vector<double> s(n);
     Mat ud(n, n);
@@ -211,6 +218,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
     if (cfg.verbose) std::printf("Running %llu iterations of FastICA...\n", (unsigned long long)cfg.fastica_it);
     w_init_ = ica_par(w_init_);
   }
+  lap(3);
   // x1 = w_init·x1 (solver.rs:140), kept as the composed map P
   P_ = has_k_ ? matmul(w_init_, K_) : w_init_;
   has_cov_ = extended_ && cfg.whiten;  // solver.rs:143-147
@@ -223,6 +231,10 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   no_multi_ = std::getenv("PICARD_NO_MULTI") != nullptr;
   split_first_ = std::getenv("PICARD_SPLIT_FIRST") != nullptr;
   init_core();
+  lap(4);
+  if (trace_)
+    std::fprintf(stderr, "[picard-trace] setup ms (cumulative): rowsum %.3f gram %.3f eigh %.3f w_init %.3f initial pass %.3f\n",
+                 tsm[0], tsm[1], tsm[2], tsm[3], tsm[4]);
 }
 
 static double now_ms() {
