@@ -4144,10 +4144,8 @@ struct DeviceCtx : Evaluator {
     int coop = 0;
     HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
     if (!coop) return false;
-    // four waves per workgroup (default) or one (PICARD_JADE_THREADS=64): the same arithmetic
-    const char* jt = std::getenv("PICARD_JADE_THREADS");
-    const int th = jt && std::atoi(jt) == 64 ? 64 : JS_THREADS;
-    const void* kern = th == 64 ? (const void*)k_jade_sweeps<64> : (const void*)k_jade_sweeps<JS_THREADS>;
+    const int th = JS_THREADS;
+    const void* kern = (const void*)k_jade_sweeps<JS_THREADS>;
     lds_attr(kern, (int)lds);
     int per_cu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, th, lds));

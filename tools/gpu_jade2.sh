@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_jade.py tests/test_gpu_parity.py -k "jade" -x -q --timeout 200 --timeout-method thread \
   > gpurun_out/pytest_jade_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_jade_$TAG.log; exit 1; }
 tail -2 gpurun_out/pytest_jade_$TAG.log
-for th in 256 64 256 64; do
+for th in 256 256; do
   PICARD_JADE_THREADS=$th PICARD_TRACE=1 timeout -k 10 200 python3 tools/run_configs.py C5 > gpurun_out/c5_$TAG.$th.json 2> gpurun_out/c5_$TAG.$th.log || exit 1
   echo "threads $th: $(grep 'jade:' gpurun_out/c5_$TAG.$th.log)"
 done
