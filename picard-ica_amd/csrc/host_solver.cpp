@@ -112,8 +112,21 @@ static int host_team_threads() {
   return v;
 }
 
+// The calling thread's OpenMP team for the solver's host work, the caller's own setting
+// restored on exit: the library leaves a caller's OpenMP state as it found it.
+class TeamGuard {
+ public:
+  explicit TeamGuard(int n) : prev_(omp_get_max_threads()) { omp_set_num_threads(n); }
+  ~TeamGuard() { omp_set_num_threads(prev_); }
+  TeamGuard(const TeamGuard&) = delete;
+  TeamGuard& operator=(const TeamGuard&) = delete;
+
+ private:
+  const int prev_;
+};
+
 Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
-  omp_set_num_threads(host_team_threads());
+  TeamGuard team(host_team_threads());
   // config.rs:104-142
   if (cfg.max_iter == 0) throw invalid_config("max_iter", "must be greater than 0");
   if (!(cfg.tol > 0.0)) throw invalid_config("tol", "must be positive");
@@ -730,6 +743,8 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
 }
 
 bool Solver::step() {
+  // with the line-search helper running, its core is taken out of the team (see line_search)
+  TeamGuard team(ahead_ ? std::max(1, host_team_threads() - 1) : host_team_threads());
   if (done_) return true;
   const double step_t0 = now_ms(), eval_t0 = eval_ms_, wait_t0 = ahead_wait_ms_;
   const size_t n = nc_;
@@ -870,6 +885,7 @@ static double* dup(const double* p, size_t n) {
 }
 
 void Solver::finish(pc_result* out) {
+  TeamGuard team(ahead_ ? std::max(1, host_team_threads() - 1) : host_team_threads());
   std::memset(out, 0, sizeof *out);
   Mat w = matmul(W_, w_init_);  // solver.rs:169
   if (!converged_ && cfg_.verbose)

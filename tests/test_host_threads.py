@@ -46,3 +46,22 @@ def test_fit_bits_independent_of_host_team(tmp_path):
     b = _fit(tmp_path, 8)
     assert a[-1] >= 2  # iterations ran (line searches, Taylor series)
     assert np.array_equal(a, b)
+
+
+def test_solver_leaves_the_callers_openmp_team(pa, po, c1_data):
+    """The solver runs its host work on its own team size (PICARD_HOST_THREADS cap) and gives the
+    calling thread back its OpenMP setting: a library call must not change the caller's team."""
+    import ctypes
+
+    gomp = ctypes.CDLL("libgomp.so.1")  # the runtime the library links (one per process)
+    x, _, _ = c1_data
+
+    def ev(w, mu, d, need_h):
+        return po.pass_stats(w, mu, x, po.Density(["tanh", "exp", "cube"][d.kind], d.alpha), need_h)
+
+    gomp.omp_set_num_threads(3)
+    r = pa.fit_with_host_evaluator(8, x.shape[1], pa.PicardConfig(w_init=np.eye(8), max_iter=20),
+                                   rowsum=lambda: x.sum(axis=1), gram=lambda mu: (x - mu[:, None]) @ (x - mu[:, None]).T,
+                                   eval=ev, sources=lambda w, mu: w @ (x - mu[:, None]))
+    assert r.n_iterations > 1
+    assert gomp.omp_get_max_threads() == 3
