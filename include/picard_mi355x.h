@@ -49,9 +49,10 @@ extern "C" {
  * eval_loss_screen slots (a caller built against revision 1 must be rebuilt), the
  * rank-group entry points (pc_group_*, pc_ctx_create_in_group, pc_ctx_comm_stats,
  * pc_ctx_abort) and pc_ctx_release_caches were added. 3: pc_ctx_eval_loss_multi_bound
- * was added (no layout change). pc_abi_version() returns the revision the library was
- * built with. */
-#define PC_ABI_VERSION 3
+ * was added (no layout change). 4: PC_ERR_UNSUPPORTED for capability misses of the
+ * operator boundary (they no longer abort a rank group). pc_abi_version() returns the
+ * revision the library was built with. */
+#define PC_ABI_VERSION 4
 
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {
@@ -60,7 +61,12 @@ typedef enum {
   PC_ERR_SINGULAR_MATRIX = 2,
   PC_ERR_COMPUTATION = 3,
   PC_ERR_INVALID_CONFIG = 4,
-  PC_ERR_NOT_CONVERGED = 5
+  PC_ERR_NOT_CONVERGED = 5,
+  /* operator boundary only (never returned by pc_fit): the requested pass or placement is
+   * not available for this context / shape / density. Nothing ran and a rank group is NOT
+   * aborted — the documented fallback (pc_ctx_eval_loss_multi, an exact try, host JADE
+   * sweeps) can be called next on every rank. */
+  PC_ERR_UNSUPPORTED = 6
 } pc_status;
 
 /* src/density.rs:137-144 DensityType */
@@ -221,7 +227,7 @@ int pc_ctx_eval_loss(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu
  * z = (D·W)·P (both nc × n_features), writes Σℓ and Σy² of
  * Y_j = (w + α_j·z)·(X − μ) for every α_j: ll_out[j·nc + i], y2_out[j·nc + i].
  * Equal to pc_ctx_eval_loss at w + α_j·z up to rounding (Y_j is formed as
- * Y + α_j·Z). Returns PC_ERR_COMPUTATION for a shape the pass does not cover
+ * Y + α_j·Z). Returns PC_ERR_UNSUPPORTED for a shape the pass does not cover
  * (nc > 256, or a negative tanh/exp α). */
 int pc_ctx_eval_loss_multi(pc_ctx* ctx, const double* w, const double* z, uint64_t nc, const double* mu,
                            pc_density density, const double* alphas, uint64_t n_alpha, double* ll_out,
@@ -231,7 +237,7 @@ int pc_ctx_eval_loss_multi(pc_ctx* ctx, const double* w, const double* z, uint64
  * non-extended fit, whose loss needs no Σy²): |Σℓ_j,i − ll_out[j·nc + i]| ≤ bnd_out[j·nc + i]
  * where Σℓ_j,i is what pc_ctx_eval_loss gives at w + α_j·z. n_alpha ≤ 12. Enabled by
  * PICARD_MULTI_F32=1 (off by default: slower end to end on C4). Returns
- * PC_ERR_COMPUTATION where it does not apply (the caller then uses pc_ctx_eval_loss_multi). */
+ * PC_ERR_UNSUPPORTED where it does not apply (the caller then uses pc_ctx_eval_loss_multi). */
 int pc_ctx_eval_loss_multi_bound(pc_ctx* ctx, const double* w, const double* z, uint64_t nc, const double* mu,
                                  pc_density density, const double* alphas, uint64_t n_alpha, double* ll_out,
                                  double* bnd_out, char* err, size_t errlen);
@@ -267,8 +273,8 @@ int pc_ctx_moments4(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu,
  * (jade.rs:78-131), up to max_iter Jacobi sweeps in the reference's cyclic
  * (p, q) order (jade.rs:37-69) with the angle tolerance tol, and
  * w_out = sym_decorrelation(V) (nc × nc, jade.rs:69). `where` places the
- * sweeps: PC_JADE_AUTO (host), PC_JADE_DEVICE (one cooperative device launch;
- * PC_ERR_COMPUTATION if the shape does not fit it) or PC_JADE_HOST.
+ * sweeps: PC_JADE_AUTO (host), PC_JADE_DEVICE (one device launch;
+ * PC_ERR_UNSUPPORTED if the shape does not fit it) or PC_JADE_HOST.
  * sweeps_out (or NULL): [0] sweeps run, [1] 1 if the tolerance was met,
  * [2] 1 if the sweeps ran on the device. */
 enum { PC_JADE_AUTO = 0, PC_JADE_DEVICE = 1, PC_JADE_HOST = 2 };
@@ -336,7 +342,7 @@ void pc_ctx_kernel_breakdown(pc_ctx* ctx, double ms[4], uint64_t n[4], int32_t r
  * fp64 MFMA Y stage. Either way the statistics agree with the fp64 oracle to
  * 1e-12 relative; they are bit-identical only within one mode.
  * Under PC_YSTAGE_AUTO the orthogonal solver also SCREENS its loss-only
- * line-search tries: a pass on the 5 leading digit diagonals (15 digit products)
+ * line-search tries: a pass on the 4 leading digit diagonals (10 digit products)
  * plus a rigorous bound on the exact Σℓ rejects a try when no exact value could
  * accept it (core.rs:127-140 decides the same way); every other try runs the
  * exact pass. PC_YSTAGE_INT8_EXACT: the int8 stage without the screen (every
@@ -345,11 +351,11 @@ enum { PC_YSTAGE_AUTO = 0, PC_YSTAGE_F64 = 1, PC_YSTAGE_INT8_EXACT = 2 };
 int pc_ctx_set_y_stage(pc_ctx* ctx, int32_t mode);
 /* number of passes whose Y stage ran on the int8 slices since the context was created */
 uint64_t pc_ctx_int8_passes(const pc_ctx* ctx);
-/* The line-search screen itself: ll_out[i] = Σℓ of row i from the 5 leading digit
+/* The line-search screen itself: ll_out[i] = Σℓ of row i from the 4 leading digit
  * diagonals, bound_out[i] ≥ |Σℓ_exact − ll_out[i]| (rounding included), both summed
- * over ranks. Returns PC_ERR_COMPUTATION when the context has no screen for this
- * shape / density (int8 stage off, nc outside (64, 128], n_features > 128, cube,
- * α ≤ 0). */
+ * over ranks. Returns PC_ERR_UNSUPPORTED when the context has no screen for this
+ * shape / density (int8 stage off, nc outside (32, 128], n_features above 64 for
+ * nc ≤ 64 or above 128, cube, α ≤ 0). */
 int pc_ctx_eval_loss_screen(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, pc_density density,
                             double* ll_out, double* bound_out, char* err, size_t errlen);
 /* line-search screen passes since the last reset: summed HIP-event kernel ms and count */
@@ -363,6 +369,8 @@ void pc_ctx_screen_stats(pc_ctx* ctx, double* kernel_ms, uint64_t* n_launches, i
 int pc_device_check_fp32_transcendentals(int32_t device, double out[4]);
 /* hipDeviceSynchronize on `device` (bench bracketing). */
 int pc_device_synchronize(int32_t device);
+/* hipMemGetInfo of `device`: free and total HBM bytes (either pointer may be NULL) */
+int pc_device_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes);
 
 #ifdef __cplusplus
 }

@@ -29,7 +29,7 @@ import numpy as np
 __all__ = [
     "Picard", "PicardConfig", "ConfigBuilder", "PicardResult", "DensityType", "PicardError",
     "InvalidDimensions", "SingularMatrix", "ComputationError", "InvalidConfig", "NotConverged",
-    "DeviceContext", "LocalGroup", "Solver", "utils", "lib", "LIB_PATH",
+    "Unsupported", "DeviceContext", "LocalGroup", "Solver", "utils", "lib", "LIB_PATH",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -64,7 +64,16 @@ class NotConverged(PicardError):
     code = 5
 
 
-_ERRORS = {c.code: c for c in (InvalidDimensions, SingularMatrix, ComputationError, InvalidConfig, NotConverged)}
+class Unsupported(ComputationError):
+    """PC_ERR_UNSUPPORTED (operator boundary only): the pass is not available for this
+    context / shape; nothing ran and a rank group is not aborted, so the documented fallback
+    can be called next. A ComputationError, so callers that catch those still do."""
+
+    code = 6
+
+
+_ERRORS = {c.code: c for c in (InvalidDimensions, SingularMatrix, ComputationError, InvalidConfig, NotConverged,
+                               Unsupported)}
 
 # ------------------------------------------------------------------ C types
 
@@ -185,6 +194,7 @@ def _load():
         "pc_ctx_last_timing": (None, [vp, d, d]),
         "pc_ctx_kernel_stats": (None, [vp, d, d, P(u64), i32]),
         "pc_device_synchronize": (C.c_int, [i32]),
+        "pc_device_mem_info": (C.c_int, [i32, P(u64), P(u64)]),
         "pc_device_check_fp32_transcendentals": (C.c_int, [i32, P(C.c_double)]),
         "pc_ctx_kernel_breakdown": (None, [vp, d, P(u64), i32]),
         "pc_ctx_set_y_stage": (C.c_int, [vp, i32]),
@@ -216,7 +226,7 @@ EXPORTED = [
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_fit_with_evaluator",
 ]
 
@@ -484,6 +494,15 @@ def device_synchronize(device: int = 0) -> None:
     rc = lib.pc_device_synchronize(device)
     if rc:
         raise ComputationError("hipDeviceSynchronize failed")
+
+
+def device_mem_info(device: int = 0) -> tuple:
+    """pc_device_mem_info: (free, total) HBM bytes of `device`."""
+    f, t = C.c_uint64(), C.c_uint64()
+    rc = lib.pc_device_mem_info(device, C.byref(f), C.byref(t))
+    if rc:
+        raise ComputationError("hipMemGetInfo failed")
+    return f.value, t.value
 
 
 def rccl_unique_id() -> bytes:

@@ -32,6 +32,7 @@ void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double*
 int rccl_unique_id(char* out);
 void device_ctx_kernel_stats(Evaluator* e, double* kernel_ms, double* call_ms, uint64_t* n, int reset);
 void device_synchronize(int device);
+void device_mem_info(int device, uint64_t* free_b, uint64_t* total_b);
 void device_check_f32_transc(int device, double* out4);
 void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset);
 void device_ctx_set_y_stage(Evaluator* e, int mode);
@@ -303,6 +304,7 @@ const char* pc_error_name(int s) {
     case PC_ERR_COMPUTATION: return "ComputationError";
     case PC_ERR_INVALID_CONFIG: return "InvalidConfig";
     case PC_ERR_NOT_CONVERGED: return "NotConverged";
+    case PC_ERR_UNSUPPORTED: return "Unsupported";
     default: return "Unknown";
   }
 }
@@ -419,7 +421,7 @@ int pc_ctx_eval_loss_multi(pc_ctx* c, const double* w, const double* z, uint64_t
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
     if (n_alpha == 0) return;
     if (!c->ev->eval_loss_multi(w, z, nc, mu, d, alphas, (int)n_alpha, ll_out, y2_out))
-      throw computation_error("multi-try loss pass not available for this shape");
+      throw unsupported("multi-try loss pass not available for this shape");
   });
 }
 
@@ -432,7 +434,7 @@ int pc_ctx_eval_loss_multi_bound(pc_ctx* c, const double* w, const double* z, ui
     if (n_alpha == 0) return;
     c->ev->want_y2 = false;
     if (!c->ev->eval_loss_multi_bound(w, z, nc, mu, d, alphas, (int)n_alpha, ll_out, bnd_out))
-      throw computation_error("bounded multi-try pass not available here");
+      throw unsupported("bounded multi-try pass not available here");
   });
 }
 
@@ -495,7 +497,7 @@ int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const doubl
                             double* ll_out, double* bound_out, char* err, size_t errlen) {
   return guarded_on(c->ev.get(), err, errlen, [&] {
     if (!c->ev->eval_loss_screen(w, nc, mu, density, ll_out, bound_out))
-      throw computation_error("no line-search screen for this shape / density");
+      throw unsupported("no line-search screen for this shape / density");
   });
 }
 
@@ -506,6 +508,15 @@ void pc_ctx_screen_stats(pc_ctx* c, double* ms, uint64_t* n, int32_t reset) {
 int pc_device_check_fp32_transcendentals(int32_t device, double out[4]) {
   try {
     device_check_f32_transc(device, out);
+    return PC_OK;
+  } catch (const PicardError& e) {
+    return e.code;
+  }
+}
+
+int pc_device_mem_info(int32_t device, uint64_t* free_bytes, uint64_t* total_bytes) {
+  try {
+    device_mem_info(device, free_bytes, total_bytes);
     return PC_OK;
   } catch (const PicardError& e) {
     return e.code;

@@ -177,12 +177,14 @@ class RcclCollective final : public Collective {
     std::memcpy(&id, uid, sizeof id);
     open_abort_word(uid);
     const ncclResult_t r = ncclCommInitRank(&comm_, world, id, rank);
+    // ncclCommInitRank is collective and every rank maps the word before calling it, so once
+    // it returns (either way) the name is no longer needed: every rank unlinks it (ENOENT is
+    // fine), which also covers the other nodes of a multi-node group and a failed init
+    if (!shm_name_.empty()) shm_unlink(shm_name_.c_str());
     if (r != ncclSuccess) {
       close_abort_word();
       throw computation_error(std::string("RCCL: ") + ncclGetErrorString(r) + " at ncclCommInitRank");
     }
-    // every rank opened the word before the (collective) init returned: the name can go
-    if (rank == 0 && !shm_name_.empty()) shm_unlink(shm_name_.c_str());
   }
   ~RcclCollective() override {
     if (comm_) (void)ncclCommDestroy(comm_);
@@ -191,8 +193,10 @@ class RcclCollective final : public Collective {
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   const char* kind() const override { return "rccl"; }
-  bool aborted() const override { return local_aborted_ || (aw_ && aw_->failed.load() != 0); }
+  bool aborted() const override { return local_aborted_.load() || (aw_ && aw_->failed.load() != 0); }
 
+  // May be called from any thread (pc_ctx_abort from a watchdog while the fit thread is in
+  // allreduce / wait): comm_ and the reason are guarded by mu_, the flag is atomic.
   void abort(const std::string& why) noexcept override {
     if (aw_) {
       int expect = 0;
@@ -202,8 +206,14 @@ class RcclCollective final : public Collective {
         aw_->why[sizeof aw_->why - 1] = 0;
       }
     }
-    if (!local_why_.size()) local_why_ = why;
-    local_aborted_ = true;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (local_why_.empty()) {
+      try {
+        local_why_ = why;
+      } catch (...) {
+      }
+    }
+    local_aborted_.store(true);
     if (comm_) {
       (void)ncclCommAbort(comm_);  // ends this rank's in-flight collectives
       comm_ = nullptr;
@@ -213,7 +223,12 @@ class RcclCollective final : public Collective {
   void allreduce(double* d, size_t n, hipStream_t stream, const char* tag) override {
     (void)tag;
     check();
-    const ncclResult_t r = ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm_, stream);
+    ncclResult_t r;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!comm_) throw computation_error("rank group aborted: " + local_why_);
+      r = ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm_, stream);
+    }
     if (r != ncclSuccess) {
       const std::string m = std::string("RCCL: ") + ncclGetErrorString(r) + " in ncclAllReduce";
       abort(m);
@@ -250,7 +265,10 @@ class RcclCollective final : public Collective {
 
  private:
   void check() {
-    if (local_aborted_) throw computation_error("rank group aborted: " + local_why_);
+    if (local_aborted_.load()) {
+      std::lock_guard<std::mutex> lk(mu_);
+      throw computation_error("rank group aborted: " + local_why_);
+    }
     if (aw_ && aw_->failed.load() != 0) {
       const std::string m = std::string(aw_->why);
       abort(m);
@@ -260,7 +278,12 @@ class RcclCollective final : public Collective {
   // RCCL async error, dead peer processes, watchdog
   void probe(double waited_s) {
     ncclResult_t ae = ncclSuccess;
-    if (comm_ && ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+    bool failed;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      failed = comm_ && ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress;
+    }
+    if (failed) {
       const std::string m = std::string("RCCL async error: ") + ncclGetErrorString(ae);
       abort(m);
       throw computation_error(m);
@@ -317,7 +340,8 @@ class RcclCollective final : public Collective {
   ncclComm_t comm_ = nullptr;
   AbortWord* aw_ = nullptr;
   std::string shm_name_;
-  bool local_aborted_ = false;
+  mutable std::mutex mu_;  // comm_, local_why_
+  std::atomic<bool> local_aborted_{false};
   std::string local_why_;
 };
 

@@ -2512,6 +2512,20 @@ static void lds_attr(const void* f, int bytes) {
   }
 }
 
+// Live device contexts per device in this process (the JADE sweeps launch plainly only when
+// their context is alone on its device; jade_sweeps_impl)
+static std::mutex g_ctx_mu;
+static std::map<int, int> g_ctx_count;
+static int ctxs_on_device(int dev) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto it = g_ctx_count.find(dev);
+  return it == g_ctx_count.end() ? 0 : it->second;
+}
+static void ctx_count_add(int dev, int d) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  g_ctx_count[dev] += d;
+}
+
 // ---------------------------------------------------------------------------
 // Device context: one GPU, one X shard, optional collective (RCCL, or an
 // in-process rank group; collective.hpp).
@@ -2593,11 +2607,13 @@ struct DeviceCtx : Evaluator {
     if (grp) coll_ = make_local_collective(std::move(grp), rank);
     else if (uid) coll_ = make_rccl_collective(rank, world, uid);
     if (const char* e = std::getenv("PICARD_TEST_PIN_DIGITS")) pin_test_ = std::atoi(e) != 0;
+    ctx_count_add(device, 1);
   }
   ~DeviceCtx() override {
+    ctx_count_add(device, -1);
     (void)hipSetDevice(device);
     coll_.reset();
-    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src})
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src, d_jade})
       if (p) (void)hipFree(p);
     for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc})  // d_wsl lies inside d_wsc's allocation
       if (p) (void)hipFree(p);
@@ -4153,21 +4169,22 @@ struct DeviceCtx : Evaluator {
     // A [npos][np] as the host built it; workgroup g loads matrices g·mw … g·mw + mw − 1
     std::vector<double> eye(n * n, 0.0);
     for (size_t i = 0; i < n; ++i) eye[i * n + i] = 1.0;
-    double *d_a = nullptr, *d_v = nullptr, *d_g = nullptr;
-    int* d_sw = nullptr;
-    HIP_OK(hipMalloc(&d_a, npos * np * sizeof(double)));
-    HIP_OK(hipMalloc(&d_v, n * n * sizeof(double)));
-    HIP_OK(hipMalloc(&d_g, 2 * G * 3 * 2 * sizeof(double)));  // [2][3][G] granules {value, seq}
-    HIP_OK(hipMalloc(&d_sw, 2 * sizeof(int)));
+    // One context-owned buffer (ensure: kept across calls, freed with the context), so an
+    // error anywhere below — a throwing HIP_OK, a refused launch — leaks nothing:
+    // [A: npos·np][V: n·n][granules: 2·3·G {value, seq} pairs][θ log: cap + 1][sweep counts]
     const int theta_cap = (int)std::min<size_t>(max_iter / 10, 1u << 16);
-    double* d_th = nullptr;
-    HIP_OK(hipMalloc(&d_th, (theta_cap + 1) * sizeof(double)));
+    const size_t off_v = npos * np, off_g = off_v + n * n, off_th = off_g + 2 * G * 3 * 2,
+                 off_sw = off_th + (size_t)theta_cap + 1, total = off_sw + 1;
+    double* base = ensure(d_jade, cap_jade, total);
+    double *d_a = base, *d_v = base + off_v, *d_g = base + off_g, *d_th = base + off_th;
+    int* d_sw = (int*)(base + off_sw);
     // granule tags start at seq0 (0; PICARD_JADE_BAR_BASE presets it, a test hook:
     // the sweeps must not depend on it)
     unsigned long long seq0 = 0;
     if (const char* e = std::getenv("PICARD_JADE_BAR_BASE")) seq0 = std::strtoull(e, nullptr, 0);
     long long max_pairs = (long long)std::min<size_t>(jade_max_pairs(), (size_t)LLONG_MAX);
     HIP_OK(hipMemsetAsync(d_g, 0, 2 * G * 3 * 2 * sizeof(double), stream));  // tags 0 ≠ any seq ≥ seq0 + 1
+    HIP_OK(hipMemsetAsync(d_sw, 0, 2 * sizeof(int), stream));
     if (A) {
       HIP_OK(hipMemcpyAsync(d_a, A, npos * np * sizeof(double), hipMemcpyHostToDevice, stream));
     } else {
@@ -4177,8 +4194,32 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_v, eye.data(), n * n * sizeof(double), hipMemcpyHostToDevice, stream));
     int np_i = (int)np, n_i = (int)n, npos_i = (int)npos, mw_i = (int)mw, it_i = (int)std::min<size_t>(max_iter, 1u << 30);
     double tol_d = tol;
-    void* args[] = {&d_a, &np_i, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_sw, &d_th, (void*)&theta_cap, &seq0, &max_pairs};
-    HIP_OK(hipLaunchCooperativeKernel(kern, dim3((unsigned)G), dim3((unsigned)th), args, (unsigned)lds, stream));
+    // The kernel needs its G workgroups co-resident (each waits for the others' granules;
+    // jade_sweeps.inc), not a grid barrier: occupancy was checked above. A context alone on its
+    // device launches it plainly; contexts that share the device (an in-process rank group, or
+    // several contexts of one process) use the cooperative launch, whose admission guarantees
+    // co-residency against each other's sweeps. (A rocprofv3-traced process that ran a
+    // cooperative launch crashed in HIP's exit handler: DESIGN.md §6.) A refused launch is not
+    // an error: the host sweeps run instead (PICARD_TEST_JADE_REFUSE=1 refuses every launch,
+    // a test hook).
+    const bool coop_launch = (coll_ && std::strcmp(coll_->kind(), "local") == 0) || ctxs_on_device(device) > 1;
+    hipError_t le = hipSuccess;
+    if (std::getenv("PICARD_TEST_JADE_REFUSE") && std::atoi(std::getenv("PICARD_TEST_JADE_REFUSE")) != 0) {
+      le = hipErrorCooperativeLaunchTooLarge;
+    } else if (coop_launch) {
+      void* args[] = {&d_a, &np_i, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_sw, &d_th, (void*)&theta_cap, &seq0, &max_pairs};
+      le = hipLaunchCooperativeKernel(kern, dim3((unsigned)G), dim3((unsigned)th), args, (unsigned)lds, stream);
+    } else {
+      k_jade_sweeps<JS_THREADS><<<dim3((unsigned)G), dim3((unsigned)th), lds, stream>>>(
+          d_a, np_i, n_i, npos_i, mw_i, it_i, tol_d, d_v, d_g, d_sw, d_th, theta_cap, seq0, max_pairs);
+      le = hipGetLastError();
+    }
+    last_jade_coop_ = coop_launch;
+    if (le != hipSuccess) {
+      (void)hipGetLastError();
+      sync();  // the queued copies into the buffer are done before it is reused
+      return false;
+    }
     int sw[2] = {0, 0};
     HIP_OK(hipMemcpyAsync(v_out, d_v, n * n * sizeof(double), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipMemcpyAsync(sw, d_sw, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
@@ -4188,9 +4229,10 @@ struct DeviceCtx : Evaluator {
     log->theta10.assign(std::min<size_t>(log->sweeps / 10, (size_t)theta_cap), 0.0);
     if (!log->theta10.empty())
       HIP_OK(hipMemcpy(log->theta10.data(), d_th, log->theta10.size() * sizeof(double), hipMemcpyDeviceToHost));
-    for (void* pf : {(void*)d_a, (void*)d_v, (void*)d_g, (void*)d_sw, (void*)d_th}) (void)hipFree(pf);
     return true;
   }
+  bool last_jade_coop_ = false;
+  double* d_jade = nullptr; size_t cap_jade = 0;  // the JADE sweeps' buffer (jade_sweeps_impl)
 
   void moments4(const double* w, size_t nc, const double* mu, double* out) override {
     HIP_OK(hipSetDevice(device));
@@ -4410,6 +4452,13 @@ void device_check_f32_transc(int device, double* out4) {
 void device_synchronize(int device) {
   HIP_OK(hipSetDevice(device));
   HIP_OK(hipDeviceSynchronize());
+}
+void device_mem_info(int device, uint64_t* free_b, uint64_t* total_b) {
+  HIP_OK(hipSetDevice(device));
+  size_t f = 0, t = 0;
+  HIP_OK(hipMemGetInfo(&f, &t));
+  if (free_b) *free_b = f;
+  if (total_b) *total_b = t;
 }
 void device_ctx_raw_eval(Evaluator* e, const double* w, size_t nc, const double* mu, int dens, double alpha,
                          bool need_h, double* stats) {

@@ -27,6 +27,9 @@ inline PicardError singular_matrix() {
 inline PicardError computation_error(const std::string& m) {
   return PicardError(PC_ERR_COMPUTATION, "Computation error: " + m);
 }
+// A capability miss of the operator boundary (pc_status PC_ERR_UNSUPPORTED): the pass is
+// not available here, nothing ran, and a rank group is not aborted (guarded_on).
+inline PicardError unsupported(const std::string& m) { return PicardError(PC_ERR_UNSUPPORTED, "Unsupported: " + m); }
 inline PicardError invalid_config(const std::string& p, const std::string& m) {
   return PicardError(PC_ERR_INVALID_CONFIG, "Invalid configuration for '" + p + "': " + m);
 }

@@ -97,20 +97,21 @@ void regularize_hessian(Mat& h, const std::vector<double>& h_off, double lambda_
 // process's CPU share leaves no core for the line-search helper and the HIP runtime threads:
 // on a 16-CPU box the one-rank-of-8 C3 shard measured host time per iteration mean 1.4-2.0 ms,
 // p90 3-5 ms with 16 threads against 0.84-0.88 / 1.1-1.2 ms with 8 (profiles/r03_h). With 8
-// ranks per node, 8 teams as wide as the node would oversubscribe it 8×. Default
-// min(OMP max threads, 8); PICARD_HOST_THREADS overrides the cap. Read once, before any
-// omp_set_num_threads of this library.
-static int host_team_threads() {
-  static const int v = [] {
-    int cap = 8;
+// ranks per node, 8 teams as wide as the node would oversubscribe it 8×. The team is
+// min(the calling thread's OMP max threads at this call, cap), cap = 8 or PICARD_HOST_THREADS;
+// only the cap is read once, so a caller's smaller setting for one fit does not shrink later
+// fits.
+static int host_team_cap() {
+  static const int cap = [] {
     if (const char* e = std::getenv("PICARD_HOST_THREADS")) {
       const int c = std::atoi(e);
-      if (c > 0) cap = c;
+      if (c > 0) return c;
     }
-    return std::max(1, std::min(omp_get_max_threads(), cap));
+    return 8;
   }();
-  return v;
+  return cap;
 }
+static int host_team_threads() { return std::max(1, std::min(omp_get_max_threads(), host_team_cap())); }
 
 // The calling thread's OpenMP team for the solver's host work, the caller's own setting
 // restored on exit: the library leaves a caller's OpenMP state as it found it.
@@ -571,6 +572,8 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           }
           sln_det(wj[j], &dsg[j], &dla[j]);
         }
+        EvalStats last_full;  // bounded: the exact pass of the LAST try, if one ran and rejected it
+        bool have_last_full = false;
         for (size_t j = 0; j < na; ++j) {
           const double a = alphas[j];
           r.w = std::move(wj[j]);
@@ -597,6 +600,10 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
                 r.step = scale(direction, a);
                 return r;
               }
+              if (j + 1 == na) {  // kept below: step() needs no second pass at the same W
+                last_full = std::move(full);
+                have_last_full = true;
+              }
             }
           } else if (loss < current_loss_) {
             evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
@@ -608,12 +615,19 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           }
           alpha = a / 2.0;
         }
-        // no try accepted: the caller evaluates the last try in full if it keeps it
-        r.stats = ls;
-        r.partial = false;
-        r.needs_full = true;
+        // no try accepted: the caller evaluates the last try in full if it keeps it — unless
+        // the bounded path already ran that pass (its exact statistics and loss are kept)
         bool singular;
-        r.loss = loss_of(ls, r.w, signs_, &singular);
+        if (have_last_full) {
+          r.stats = std::move(last_full);
+          r.needs_full = false;
+          r.loss = loss_of(r.stats, r.w, signs_, &singular, dsg[na - 1], dla[na - 1]);
+        } else {
+          r.stats = ls;
+          r.needs_full = true;
+          r.loss = loss_of(ls, r.w, signs_, &singular);
+        }
+        r.partial = false;
         r.step = scale(direction, alpha);
         return r;
       }
@@ -1046,7 +1060,7 @@ Mat jade_warm_start(Evaluator* ev, const Mat& base, size_t n, const double* mu, 
   if (where == JADE_SWEEPS_DEVICE || where == JADE_SWEEPS_AUTO_DEVICE) {
     JadeSweepLog log;
     if (ev->jade_sweeps(A.data(), n, max_iter, tol, v.data(), &log)) return device_done(log, v);
-    if (where == JADE_SWEEPS_DEVICE) throw computation_error("device JADE sweeps not supported for this shape");
+    if (where == JADE_SWEEPS_DEVICE) throw unsupported("device JADE sweeps not supported for this shape");
   }
   // Sweeps in the reference's cyclic (p, q) order. The np matrices are split
   // into NCH fixed chunks; each thread rotates its chunks and forms their

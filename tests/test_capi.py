@@ -93,5 +93,8 @@ def test_result_helpers_match_oracle(pa, po):
 
 
 def test_error_names(pa):
-    assert [pa.lib.pc_error_name(i).decode() for i in range(6)] == [
-        "Ok", "InvalidDimensions", "SingularMatrix", "ComputationError", "InvalidConfig", "NotConverged"]
+    assert [pa.lib.pc_error_name(i).decode() for i in range(7)] == [
+        "Ok", "InvalidDimensions", "SingularMatrix", "ComputationError", "InvalidConfig", "NotConverged",
+        "Unsupported"]
+    assert pa.lib.pc_abi_version() == 4
+    assert issubclass(pa.Unsupported, pa.ComputationError) and pa.Unsupported.code == 6

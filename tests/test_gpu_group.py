@@ -219,6 +219,45 @@ def test_group_divergent_collectives_fail_fast(pa):
     assert any("diverged" in str(e) for e in err)
 
 
+def test_group_unsupported_is_not_an_abort(pa, monkeypatch):
+    """A capability miss (PC_ERR_UNSUPPORTED: the bounded multi-try pass with PICARD_MULTI_F32
+    unset, a screen for a density without one, device JADE sweeps for a shape that does not
+    fit) leaves the group usable: the documented fallback (pc_ctx_eval_loss_multi, an exact
+    try) then runs on every rank and matches world = 1."""
+    monkeypatch.delenv("PICARD_MULTI_F32", raising=False)
+    nf, T = 96, 40009
+    full = pa.DeviceContext(0)
+    full.generate(nf, T, 11)
+    rng = np.random.default_rng(3)
+    w = np.linalg.qr(rng.normal(size=(nf, nf)))[0]
+    z = rng.normal(size=(nf, nf)) / np.sqrt(nf)
+    mu = full.rowsum() / T
+    al = np.array([1.0, 0.5, 0.25])
+    want_ll, want_y2 = full.eval_loss_multi(w, z, al, mu, pa.DensityType.tanh())
+    full.close()
+
+    def body(r, c):
+        misses = 0
+        for call in (lambda: c.eval_loss_multi_bound(w, z, al, mu, pa.DensityType.tanh()),
+                     lambda: c.eval_loss_screen(w, mu, pa.DensityType.cube())):
+            try:
+                call()
+            except pa.Unsupported:
+                misses += 1
+        ll, y2 = c.eval_loss_multi(w, z, al, mu, pa.DensityType.tanh())
+        return misses, ll, y2, c.comm_stats()
+
+    g = RankGroup(pa, 2, nf, T, seed=11)
+    try:
+        res, err = g.run(body, timeout=120)
+    finally:
+        g.close()
+    _no_errors(err)
+    for misses, ll, y2, st in res:
+        assert misses == 2 and not st["aborted"]
+        assert rel_err(ll, want_ll) <= TOL and rel_err(y2, want_y2) <= TOL
+
+
 def test_group_refuses_bad_rank(pa):
     g = pa.LocalGroup(2)
     with pytest.raises(pa.InvalidDimensions):

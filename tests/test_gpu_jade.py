@@ -4,7 +4,7 @@ JADE (src/jade.rs:22-197) is three stages; each is checked at N = 64:
   * the fourth-moment pass (pc_ctx_moments4, MFMA) against numpy z·zᵀ of the
     pair products z = (y_i y_j)_{i≤j}, relative 1e-12 (summation order only);
   * the Jacobi sweeps — host (rotated cumulant matrices VᵀMV updated per Givens
-    pair, O(n) per matrix) and device (one cooperative launch) — against the
+    pair, O(n) per matrix) and device (one launch) — against the
     oracle's literal form (oracle.picard_oracle.jade_sweeps_batched: every
     b = v_pᵀ M v_q recomputed from V per pair, jade.rs:137-167, vectorised over
     the 2080 matrices, same cyclic pair order). The sweeps amplify rounding
@@ -86,6 +86,33 @@ def test_jade_sequence_base_independent(c5_small, monkeypatch):
     monkeypatch.setenv("PICARD_JADE_BAR_BASE", str(2 ** 32 - 5000))
     w1 = ctx.jade(k, mu, max_iter=2, where="device")[0]
     assert np.array_equal(w0, w1)
+
+
+def test_jade_refused_launch_leaks_nothing(pa, c5_small, c1_data, monkeypatch):
+    """The device sweeps' buffers are the context's (one ensure()d allocation, reused), so a
+    refused launch (PICARD_TEST_JADE_REFUSE, a test hook) leaks nothing: where='device' then
+    raises Unsupported — not an abort — and HBM free memory is the same after 1 and 10 such
+    calls; a fit (device sweeps by default) falls back to the host sweeps, bit-identical to a
+    fit that asked for them (PICARD_HOST_JADE)."""
+    ctx, k, mu, _, _ = c5_small
+    monkeypatch.setenv("PICARD_JADE_MAX_PAIRS", str(PREFIX))
+    wh = ctx.jade(k, mu, max_iter=1, where="host")[0]
+    monkeypatch.setenv("PICARD_TEST_JADE_REFUSE", "1")
+    free = []
+    for _ in range(10):
+        with pytest.raises(pa.Unsupported):
+            ctx.jade(k, mu, max_iter=1, where="device")
+        free.append(pa.device_mem_info(0)[0])
+    assert free[-1] == free[0], free
+    w, _, _, on_dev = ctx.jade(k, mu, max_iter=1)
+    assert not on_dev and np.array_equal(w, wh)
+    x = c1_data[0]
+    cfg = pa.PicardConfig(jade_it=5, max_iter=3, w_init=np.eye(x.shape[0]))
+    refused = pa.Picard.fit_with_config(x, cfg)
+    monkeypatch.delenv("PICARD_TEST_JADE_REFUSE")
+    monkeypatch.setenv("PICARD_HOST_JADE", "1")
+    host = pa.Picard.fit_with_config(x, cfg)
+    assert np.array_equal(refused.unmixing, host.unmixing)
 
 
 @pytest.mark.parametrize("host", [False, True])
