@@ -23,7 +23,9 @@ window depends on which iterations it holds (line searches that fail all 10
 tries cluster in iterations 2–16), so the default window is every iteration
 after the first up to convergence (--warmup 1 --steps 40: 36 timed steps at C3,
 `steps` in the line says how many ran). On one GPU the other BASELINE configs (C2, C4, C5) then run end to end
-(--configs 0 skips them) as extra keys. rank 0 prints one JSON line.
+(--configs 0 skips them) as extra keys. rank 0 prints one JSON line; its `ranks` list holds
+every rank's window, host ms per step (mean / p90 / max), ms inside all-reduces and their
+count (rank_entry), so a multi-GPU line says where a rank lost its time.
 """
 from __future__ import annotations
 
@@ -173,6 +175,41 @@ def cpu_baseline_jade(n: int, t_slice: int, t_full: int, seed: int, sweeps: int 
                       f"+ {sweeps} sweep(s) of {n * (n - 1) // 2} Givens pairs ({t_sw:.2f}s each, x{jade_it})"}
 
 
+def rank_entry(rank: int, window_s: float, step_ms, host_ms, eval_ms, allreduce_ms: float, allreduces: int) -> dict:
+    """One rank's view of the timed window (per-rank report of a multi-GPU run): where a
+    sub-linear curve loses its time — host spikes (host ms per step: mean / p90 / max), the
+    collectives (ms inside all-reduces, which include waiting for the slowest rank), or the
+    passes themselves (ms in pass calls)."""
+    h = np.asarray(host_ms, dtype=float) if len(host_ms) else np.zeros(1)
+    return {"rank": int(rank), "window_s": float(window_s), "steps": len(step_ms),
+            "step_ms_mean": float(np.mean(step_ms)) if len(step_ms) else None,
+            "step_ms_max": float(np.max(step_ms)) if len(step_ms) else None,
+            "host_ms_mean": float(np.mean(h)), "host_ms_p90": float(np.percentile(h, 90)), "host_ms_max": float(np.max(h)),
+            "eval_ms_per_step": float(np.sum(eval_ms) / max(len(eval_ms), 1)),
+            "allreduce_ms": float(allreduce_ms), "allreduce_ms_per_step": float(allreduce_ms / max(len(step_ms), 1)),
+            "allreduces": int(allreduces)}
+
+
+def gather_ranks(dist, entry: dict) -> list:
+    """Every rank's rank_entry, in rank order, on every rank (gloo object all-gather; a
+    single process returns [entry])."""
+    if dist is None:
+        return [entry]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, entry)
+    return sorted(out, key=lambda e: e["rank"])
+
+
+def visible_gpus() -> int:
+    """GPUs this process may use, without initialising HIP (torch.cuda.device_count does not
+    on this image; HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES narrow it)."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:
+        return 0
+
+
 def relaunch_distributed(gpus: int) -> int:
     """`python bench.py --gpus N` without a launcher: run the same command under
     torch.distributed.run (one rank per GPU) as a child process — before anything
@@ -189,6 +226,10 @@ def relaunch_distributed(gpus: int) -> int:
 
 def main():
     args = parse()
+    if args.gpus > 1:  # fail fast, before a relaunch or any rank touches a GPU
+        have = visible_gpus()
+        if args.gpus > have or int(os.environ.get("WORLD_SIZE", args.gpus)) > have:
+            sys.exit(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible to this process")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch_distributed(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
@@ -237,6 +278,9 @@ def main():
     int8_before = ctx.int8_passes
     ctx.screen_stats(reset=True)
     passes = 0
+    ar0 = ctx.comm_timing()
+    ar_issued0 = ctx.comm_stats()["allreduces"]
+    step_ms, host_ms, eval_ms = [], [], []
     t0 = time.perf_counter()
     steps_run = 0
     for _ in range(args.steps):
@@ -246,10 +290,18 @@ def main():
         lp = solver.last()[2]
         if done and lp == 0:
             break  # the convergence check alone (core.rs:289-293): no pass, not an iteration's work
+        tm = solver.timing()
+        step_ms.append(tm["step_ms"])
+        host_ms.append(tm["host_ms"])
+        eval_ms.append(tm["eval_ms"])
         passes += lp
         steps_run += 1
     barrier()
     elapsed = time.perf_counter() - t0
+    ar1 = ctx.comm_timing()
+    ranks = gather_ranks(dist, rank_entry(rank, elapsed, step_ms, host_ms, eval_ms,
+                                          ar1["allreduce_ms"] - ar0["allreduce_ms"],
+                                          ctx.comm_stats()["allreduces"] - ar_issued0))
     _, call_ms, _ = ctx.kernel_stats(reset=False)
     brk = ctx.kernel_breakdown(reset=False)
     int8_timed = ctx.int8_passes - int8_before
@@ -372,6 +424,7 @@ def main():
                        "note": "all iterations to tol (warmup + timed + rest); window-independent"}
                       if iters_to_tol else None),
         "ms_in_eval_calls_per_step": call_ms / steps,
+        "ranks": ranks,
         "kernels_per_step": {k: {"ms": v[0] / steps, "launches": v[1] / steps,
                                  "avg_ms": (v[0] / v[1]) if v[1] else None} for k, v in brk.items()},
         "roofline": roof,

@@ -50,9 +50,10 @@ extern "C" {
  * rank-group entry points (pc_group_*, pc_ctx_create_in_group, pc_ctx_comm_stats,
  * pc_ctx_abort) and pc_ctx_release_caches were added. 3: pc_ctx_eval_loss_multi_bound
  * was added (no layout change). 4: PC_ERR_UNSUPPORTED for capability misses of the
- * operator boundary (they no longer abort a rank group). pc_abi_version() returns the
+ * operator boundary (they no longer abort a rank group). 5: pc_ctx_comm_timing,
+ * pc_solver_timing, pc_device_mem_info. pc_abi_version() returns the
  * revision the library was built with. */
-#define PC_ABI_VERSION 4
+#define PC_ABI_VERSION 5
 
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {
@@ -172,6 +173,10 @@ int pc_ctx_create_in_group(int32_t device, int32_t rank, pc_group* g, pc_ctx** o
  * [4] 1 once the group was aborted, [5] world size, [6] 1 RCCL, 2 in-process group,
  * 0 none. */
 void pc_ctx_comm_stats(const pc_ctx* ctx, int64_t out[7]);
+/* Time inside the context's all-reduces since it was created: out[0] ms (RCCL: device time
+ * between HIP events around each ncclAllReduce, which includes waiting for the slowest rank;
+ * in-process group: host time of the exchange), out[1] the number of all-reduces timed. */
+void pc_ctx_comm_timing(const pc_ctx* ctx, double out[2]);
 /* Abort the context's rank group: every rank's pending and later collectives (RCCL:
  * through ncclCommAbort and a shared abort word the peers poll while they wait) end
  * with PC_ERR_COMPUTATION. Any pc_ctx_* / pc_solver_* call that fails with
@@ -293,6 +298,10 @@ int pc_solver_finish(pc_solver* s, pc_result* out, char* err, size_t errlen);
 void pc_solver_destroy(pc_solver* s);
 /* last iteration's: loss, gradient norm, passes issued in that iteration */
 void pc_solver_last(const pc_solver* s, double* loss, double* gradient_norm, uint64_t* n_evals);
+/* last iteration's timing: out[0] wall ms, [1] ms inside pass calls (device work, all-reduces,
+ * waits), [2] host ms (the rest: the N×N work of core.rs), [3] ms waiting for the line-search
+ * helper thread */
+void pc_solver_timing(const pc_solver* s, double out[4]);
 
 /* Host-driver hook: run the same solver pipeline over caller-supplied
  * evaluation callbacks instead of the HIP context. Used by the CPU test suite

@@ -19,6 +19,7 @@ std::shared_ptr<LocalGroup> make_local_group(int world);
 int local_group_world(const LocalGroup& g);
 Evaluator* make_device_ctx(int device, int rank, int world, const char* uid, std::shared_ptr<LocalGroup> grp);
 void device_ctx_comm_stats(const Evaluator* e, int64_t* out);
+void device_ctx_comm_timing(const Evaluator* e, double* out);
 void device_ctx_release_caches(Evaluator* e);
 void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0);
 void device_ctx_generate(Evaluator* e, uint64_t nf, uint64_t nt, uint64_t seed, double* a_out);
@@ -359,6 +360,7 @@ int pc_ctx_create_in_group(int32_t device, int32_t rank, pc_group* g, pc_ctx** o
 }
 
 void pc_ctx_comm_stats(const pc_ctx* c, int64_t out[7]) { device_ctx_comm_stats(c->ev.get(), out); }
+void pc_ctx_comm_timing(const pc_ctx* c, double out[2]) { device_ctx_comm_timing(c->ev.get(), out); }
 
 void pc_ctx_abort(pc_ctx* c, const char* why) { c->ev->abort_group(why ? why : "aborted by the caller"); }
 
@@ -587,6 +589,8 @@ int pc_solver_finish(pc_solver* s, pc_result* out, char* err, size_t errlen) {
 }
 
 void pc_solver_destroy(pc_solver* s) { delete s; }
+
+void pc_solver_timing(const pc_solver* s, double out[4]) { s->s->last_timing(out); }
 
 void pc_solver_last(const pc_solver* s, double* loss, double* gn, uint64_t* n_evals) {
   if (loss) *loss = s->s->last_loss();

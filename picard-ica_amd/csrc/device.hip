@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -2618,6 +2619,9 @@ struct DeviceCtx : Evaluator {
     for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc})  // d_wsl lies inside d_wsc's allocation
       if (p) (void)hipFree(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& pr : ar_ev_)
+      for (auto& e : pr)
+        if (e) (void)hipEventDestroy(e);
     for (PinSlot* sl : {&pin_w_, &pin_wsl_, &pin_out_, &pin_in_, &pin_direct_}) {
       if (sl->pending) (void)hipEventSynchronize(sl->ev);
       if (sl->p) (void)hipHostFree(sl->p);
@@ -2635,8 +2639,33 @@ struct DeviceCtx : Evaluator {
   }
   // wait for this context's stream; with a collective, a failing peer ends the wait
   void sync() {
-    if (coll_) coll_->wait(stream);
-    else HIP_OK(hipStreamSynchronize(stream));
+    if (coll_) {
+      coll_->wait(stream);
+      harvest_allreduce_timing();
+    } else {
+      HIP_OK(hipStreamSynchronize(stream));
+    }
+  }
+  // Time inside the all-reduces (bench.py's per-rank report): RCCL — device time between HIP
+  // events around each ncclAllReduce on the stream (the kernel waits there for the slowest
+  // rank); in-process group — host time of the exchange. Events come from a ring, read back
+  // at the next sync.
+  static constexpr int AR_RING = 16;
+  hipEvent_t ar_ev_[AR_RING][2] = {};
+  int ar_pending_ = 0;
+  double ar_ms_ = 0.0;
+  uint64_t ar_timed_ = 0;
+  void harvest_allreduce_timing() {
+    for (int i = 0; i < ar_pending_; ++i) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, ar_ev_[i][0], ar_ev_[i][1]) == hipSuccess) {
+        ar_ms_ += ms;
+        ++ar_timed_;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+    ar_pending_ = 0;
   }
 
   double* ensure(double*& p, size_t& cap, size_t n) {
@@ -2726,7 +2755,25 @@ struct DeviceCtx : Evaluator {
   }
 
   void allreduce(double* d, size_t n, const char* tag) {
-    if (coll_) coll_->allreduce(d, n, stream, tag);
+    if (!coll_) return;
+    if (std::strcmp(coll_->kind(), "rccl") != 0) {
+      const auto t0 = std::chrono::steady_clock::now();
+      coll_->allreduce(d, n, stream, tag);
+      ar_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      ++ar_timed_;
+      return;
+    }
+    if (ar_pending_ == AR_RING) {  // ring full before a sync: wait for the oldest pairs
+      HIP_OK(hipEventSynchronize(ar_ev_[AR_RING - 1][1]));
+      harvest_allreduce_timing();
+    }
+    hipEvent_t* e = ar_ev_[ar_pending_];
+    for (int k = 0; k < 2; ++k)
+      if (!e[k]) HIP_OK(hipEventCreate(&e[k]));
+    HIP_OK(hipEventRecord(e[0], stream));
+    coll_->allreduce(d, n, stream, tag);
+    HIP_OK(hipEventRecord(e[1], stream));
+    ++ar_pending_;
   }
 
   // ---- Y = W·Xs stored row-major on MFMA (k_ystore) ------------------------
@@ -4370,6 +4417,12 @@ void device_ctx_comm_stats(const Evaluator* e, int64_t* out) {
   out[4] = d->coll_ && d->coll_->aborted() ? 1 : 0;
   out[5] = d->world;
   out[6] = !d->coll_ ? 0 : std::strcmp(d->coll_->kind(), "rccl") == 0 ? 1 : 2;
+}
+// [0] ms inside all-reduces (see DeviceCtx::allreduce), [1] all-reduces timed
+void device_ctx_comm_timing(const Evaluator* e, double* out) {
+  auto* d = static_cast<const DeviceCtx*>(e);
+  out[0] = d->ar_ms_;
+  out[1] = (double)d->ar_timed_;
 }
 // drop the HBM caches (int8 digit image, kept-Y buffer): later passes run without them
 void device_ctx_release_caches(Evaluator* e) {

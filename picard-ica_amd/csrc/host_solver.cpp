@@ -867,6 +867,13 @@ bool Solver::step() {
     bool singular;
     res.loss = loss_of(res.stats, res.w, signs_, &singular);
   }
+  {
+    const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
+    last_timing_[0] = step_ms;
+    last_timing_[1] = dev_ms;
+    last_timing_[2] = step_ms - dev_ms;
+    last_timing_[3] = ahead_wait_ms_ - wait_t0;
+  }
   if (trace_) {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"

@@ -50,6 +50,12 @@ class Solver {
   double last_loss() const { return current_loss_; }
   double last_gnorm() const { return gradient_norm_; }
   uint64_t last_evals() const { return last_evals_; }
+  // the last step(): [0] wall ms, [1] ms inside evaluator calls (device passes, their
+  // all-reduces and waits), [2] host ms (the rest: N×N work), [3] ms waiting for the
+  // line-search helper thread's maps
+  void last_timing(double out[4]) const {
+    for (int i = 0; i < 4; ++i) out[i] = last_timing_[i];
+  }
   uint64_t total_evals() const { return total_evals_; }
   uint64_t total_completions() const { return total_completions_; }
   uint64_t screen_passes() const { return screen_passes_; }
@@ -100,6 +106,7 @@ class Solver {
   double gradient_norm_ = 1.0;
   bool converged_ = false, done_ = false;
   uint64_t last_evals_ = 0, total_evals_ = 0;
+  double last_timing_[4] = {0.0, 0.0, 0.0, 0.0};
   uint64_t total_completions_ = 0;
   uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
   bool screen_ok_ = true;  // false once the evaluator declined a screen (then never asked again)

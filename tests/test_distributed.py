@@ -116,3 +116,58 @@ def test_shard_partition_covers_all():
             assert sum(n for _, n in parts) == T
             for (t0, n), (t1, _) in zip(parts, parts[1:]):
                 assert t0 + n == t1
+
+
+def _rank_report_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        # synthetic per-step timings of a 5-step window: rank r has a host spike of 10·(r + 1) ms
+        host = [1.0, 1.2, 10.0 * (rank + 1), 0.9, 1.1]
+        step = [20.0 + h for h in host]
+        ev = [19.0] * 5
+        ranks = bench.gather_ranks(dist, bench.rank_entry(rank, 0.1 + rank, step, host, ev, 3.5 * (rank + 1), 11))
+        q.put((rank, ranks))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_bench_rank_report_gathers_every_rank():
+    """bench.py's per-rank report: rank_entry summarises a rank's window
+    and gather_ranks all-gathers the entries over the process group (gloo here, as bench.py
+    does beside RCCL), so rank 0's JSON line holds every rank's window, host ms per step
+    (mean / p90 / max), ms inside all-reduces and their count."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_rank_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]  # every rank holds the same list
+    ranks = res[0]
+    assert [e["rank"] for e in ranks] == [0, 1]
+    for r, e in enumerate(ranks):
+        assert e["window_s"] == pytest.approx(0.1 + r) and e["steps"] == 5
+        assert e["host_ms_max"] == pytest.approx(10.0 * (r + 1))
+        assert e["host_ms_mean"] == pytest.approx((1.0 + 1.2 + 10.0 * (r + 1) + 0.9 + 1.1) / 5)
+        assert e["host_ms_p90"] <= e["host_ms_max"]
+        assert e["allreduce_ms"] == pytest.approx(3.5 * (r + 1)) and e["allreduces"] == 11
+        assert e["allreduce_ms_per_step"] == pytest.approx(3.5 * (r + 1) / 5)
+        assert e["eval_ms_per_step"] == pytest.approx(19.0)
+
+
+def test_bench_single_process_report():
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    e = bench.rank_entry(0, 1.0, [], [], [], 0.0, 0)
+    assert bench.gather_ranks(None, e) == [e] and e["steps"] == 0
