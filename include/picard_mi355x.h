@@ -51,7 +51,8 @@ extern "C" {
  * pc_ctx_abort) and pc_ctx_release_caches were added. 3: pc_ctx_eval_loss_multi_bound
  * was added (no layout change). 4: PC_ERR_UNSUPPORTED for capability misses of the
  * operator boundary (they no longer abort a rank group). 5: pc_ctx_comm_timing,
- * pc_solver_timing, pc_device_mem_info. pc_abi_version() returns the
+ * pc_solver_timing, pc_solver_setup_timing, pc_ctx_alloc_stats, pc_last_teardown,
+ * pc_device_mem_info. pc_abi_version() returns the
  * revision the library was built with. */
 #define PC_ABI_VERSION 5
 
@@ -177,6 +178,13 @@ void pc_ctx_comm_stats(const pc_ctx* ctx, int64_t out[7]);
  * between HIP events around each ncclAllReduce, which includes waiting for the slowest rank;
  * in-process group: host time of the exchange), out[1] the number of all-reduces timed. */
 void pc_ctx_comm_timing(const pc_ctx* ctx, double out[2]);
+/* HBM allocation calls of the context so far: out[0..2] ms spent in hipMalloc / hipFree /
+ * hipMemGetInfo, out[3..5] their counts, out[6..8] the longest single call of each. */
+void pc_ctx_alloc_stats(const pc_ctx* ctx, double out[9]);
+/* The last context teardown in this process (pc_ctx_destroy): out[0] wall ms, [1] ms in its
+ * hipFree calls, [2] the longest single hipFree of that context's life, [3] ms of the closing
+ * hipDeviceSynchronize (deferred work of the frees is charged to the teardown). */
+void pc_last_teardown(double out[4]);
 /* Abort the context's rank group: every rank's pending and later collectives (RCCL:
  * through ncclCommAbort and a shared abort word the peers poll while they wait) end
  * with PC_ERR_COMPUTATION. Any pc_ctx_* / pc_solver_* call that fails with
@@ -302,6 +310,9 @@ void pc_solver_last(const pc_solver* s, double* loss, double* gradient_norm, uin
  * waits), [2] host ms (the rest: the N×N work of core.rs), [3] ms waiting for the line-search
  * helper thread */
 void pc_solver_timing(const pc_solver* s, double out[4]);
+/* the solver's setup phases, ms since pc_solver_create started (cumulative): out[0] row sums,
+ * [1] Gram, [2] eigh, [3] w_init + warm start, [4] the initial pass */
+void pc_solver_setup_timing(const pc_solver* s, double out[5]);
 
 /* Host-driver hook: run the same solver pipeline over caller-supplied
  * evaluation callbacks instead of the HIP context. Used by the CPU test suite

@@ -171,6 +171,8 @@ def _load():
         "pc_ctx_create_in_group": (C.c_int, [i32, i32, vp, P(vp), cp, sz]),
         "pc_ctx_comm_stats": (None, [vp, P(C.c_int64)]),
         "pc_ctx_comm_timing": (None, [vp, d]),
+        "pc_ctx_alloc_stats": (None, [vp, d]),
+        "pc_last_teardown": (None, [d]),
         "pc_ctx_abort": (None, [vp, cp]),
         "pc_ctx_release_caches": (C.c_int, [vp, cp, sz]),
         "pc_rccl_unique_id": (C.c_int, [cp]),
@@ -208,6 +210,7 @@ def _load():
         "pc_solver_destroy": (None, [vp]),
         "pc_solver_last": (None, [vp, d, d, P(u64)]),
         "pc_solver_timing": (None, [vp, d]),
+        "pc_solver_setup_timing": (None, [vp, d]),
         "pc_fit_with_evaluator": (C.c_int, [P(_HostEvaluator), P(_Config), P(_Result), cp, sz]),
     }
     for name, (res, args) in sigs.items():
@@ -224,12 +227,12 @@ EXPORTED = [
     "pc_config_default", "pc_config_validate", "pc_fit", "pc_fit_default", "pc_transform",
     "pc_full_unmixing", "pc_mixing", "pc_result_free", "pc_amari_distance", "pc_permute",
     "pc_error_name", "pc_version", "pc_abi_version", "pc_rccl_unique_id", "pc_ctx_create", "pc_ctx_destroy",
-    "pc_group_create_local", "pc_group_destroy", "pc_ctx_create_in_group", "pc_ctx_comm_stats", "pc_ctx_comm_timing", "pc_ctx_abort",
+    "pc_group_create_local", "pc_group_destroy", "pc_ctx_create_in_group", "pc_ctx_comm_stats", "pc_ctx_comm_timing", "pc_ctx_alloc_stats", "pc_last_teardown", "pc_ctx_abort",
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
     "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
-    "pc_solver_destroy", "pc_solver_last", "pc_solver_timing", "pc_fit_with_evaluator",
+    "pc_solver_destroy", "pc_solver_last", "pc_solver_timing", "pc_solver_setup_timing", "pc_fit_with_evaluator",
 ]
 
 
@@ -507,6 +510,14 @@ def device_mem_info(device: int = 0) -> tuple:
     return f.value, t.value
 
 
+def last_teardown() -> dict:
+    """pc_last_teardown: the last pc_ctx_destroy's wall ms, ms in hipFree, longest hipFree,
+    ms of the closing device synchronisation."""
+    o = (C.c_double * 4)()
+    lib.pc_last_teardown(o)
+    return {"wall_ms": o[0], "free_ms": o[1], "max_free_ms": o[2], "sync_ms": o[3]}
+
+
 def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     if lib.pc_rccl_unique_id(buf) != 0:
@@ -571,6 +582,13 @@ class DeviceContext:
         o = (C.c_double * 2)()
         lib.pc_ctx_comm_timing(self.h, o)
         return {"allreduce_ms": o[0], "allreduces_timed": int(o[1])}
+
+    def alloc_stats(self) -> dict:
+        """pc_ctx_alloc_stats: ms / count / longest call of hipMalloc, hipFree, hipMemGetInfo."""
+        o = (C.c_double * 9)()
+        lib.pc_ctx_alloc_stats(self.h, o)
+        return {k: {"ms": o[i], "calls": int(o[3 + i]), "max_ms": o[6 + i]}
+                for i, k in enumerate(("malloc", "free", "meminfo"))}
 
     def abort(self, why: str = "aborted by the caller"):
         """pc_ctx_abort: end every rank's pending and later collectives with an error."""
@@ -821,6 +839,12 @@ class Solver:
         loss, gn, ne = C.c_double(), C.c_double(), C.c_uint64()
         lib.pc_solver_last(self.h, C.byref(loss), C.byref(gn), C.byref(ne))
         return loss.value, gn.value, ne.value
+
+    def setup_timing(self) -> dict:
+        """pc_solver_setup_timing: cumulative ms of the setup phases."""
+        o = (C.c_double * 5)()
+        lib.pc_solver_setup_timing(self.h, o)
+        return dict(zip(("rowsum_ms", "gram_ms", "eigh_ms", "w_init_ms", "initial_pass_ms"), list(o)))
 
     def timing(self) -> dict:
         """pc_solver_timing: the last step's wall / in-pass / host / helper-wait ms."""

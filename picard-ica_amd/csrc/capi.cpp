@@ -20,6 +20,8 @@ int local_group_world(const LocalGroup& g);
 Evaluator* make_device_ctx(int device, int rank, int world, const char* uid, std::shared_ptr<LocalGroup> grp);
 void device_ctx_comm_stats(const Evaluator* e, int64_t* out);
 void device_ctx_comm_timing(const Evaluator* e, double* out);
+void device_ctx_alloc_stats(const Evaluator* e, double* out);
+void device_last_teardown(double* out);
 void device_ctx_release_caches(Evaluator* e);
 void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0);
 void device_ctx_generate(Evaluator* e, uint64_t nf, uint64_t nt, uint64_t seed, double* a_out);
@@ -361,6 +363,8 @@ int pc_ctx_create_in_group(int32_t device, int32_t rank, pc_group* g, pc_ctx** o
 
 void pc_ctx_comm_stats(const pc_ctx* c, int64_t out[7]) { device_ctx_comm_stats(c->ev.get(), out); }
 void pc_ctx_comm_timing(const pc_ctx* c, double out[2]) { device_ctx_comm_timing(c->ev.get(), out); }
+void pc_ctx_alloc_stats(const pc_ctx* c, double out[9]) { device_ctx_alloc_stats(c->ev.get(), out); }
+void pc_last_teardown(double out[4]) { device_last_teardown(out); }
 
 void pc_ctx_abort(pc_ctx* c, const char* why) { c->ev->abort_group(why ? why : "aborted by the caller"); }
 
@@ -422,6 +426,7 @@ int pc_ctx_eval_loss_multi(pc_ctx* c, const double* w, const double* z, uint64_t
     if (d.kind < 0 || d.kind > PC_DENSITY_CUBE) throw invalid_config("density", "unknown density kind");
     if (nc == 0 || nc > c->ev->n_features()) throw invalid_dimensions("nc must be in 1..=n_features");
     if (n_alpha == 0) return;
+    c->ev->want_y2 = true;  // this entry point returns Σy² (an earlier call may have turned it off)
     if (!c->ev->eval_loss_multi(w, z, nc, mu, d, alphas, (int)n_alpha, ll_out, y2_out))
       throw unsupported("multi-try loss pass not available for this shape");
   });
@@ -591,6 +596,7 @@ int pc_solver_finish(pc_solver* s, pc_result* out, char* err, size_t errlen) {
 void pc_solver_destroy(pc_solver* s) { delete s; }
 
 void pc_solver_timing(const pc_solver* s, double out[4]) { s->s->last_timing(out); }
+void pc_solver_setup_timing(const pc_solver* s, double out[5]) { s->s->setup_timing(out); }
 
 void pc_solver_last(const pc_solver* s, double* loss, double* gn, uint64_t* n_evals) {
   if (loss) *loss = s->s->last_loss();

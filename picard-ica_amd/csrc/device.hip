@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "collective.hpp"
+#include "screen2.hpp"
 #include "evaluator.hpp"
 #include "host_linalg.hpp"
 
@@ -2513,6 +2514,11 @@ static void lds_attr(const void* f, int bytes) {
   }
 }
 
+// The last DeviceCtx teardown: [0] wall ms, [1] ms in its hipFree calls, [2] the largest
+// single hipFree of the context's life, [3] ms of the closing hipDeviceSynchronize
+static std::mutex g_teardown_mu;
+static double g_teardown[4] = {0, 0, 0, 0};
+
 // Live device contexts per device in this process (the JADE sweeps launch plainly only when
 // their context is alone on its device; jade_sweeps_impl)
 static std::mutex g_ctx_mu;
@@ -2532,6 +2538,24 @@ static void ctx_count_add(int dev, int d) {
 // in-process rank group; collective.hpp).
 // ---------------------------------------------------------------------------
 struct DeviceCtx : Evaluator {
+  // Timed HBM allocation calls (a 6 s stall in the first setup after a
+  // large context was freed): [0] hipMalloc, [1] hipFree, [2] hipMemGetInfo — total ms, count,
+  // largest single call. pc_ctx_alloc_stats; the destructor's own record: pc_last_teardown.
+  struct AllocStats { double ms[3] = {0, 0, 0}, mx[3] = {0, 0, 0}; uint64_t n[3] = {0, 0, 0}; };
+  AllocStats as_;
+  template <class F>
+  hipError_t timed_call(int k, F&& f) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = f();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    as_.ms[k] += ms;
+    as_.mx[k] = std::max(as_.mx[k], ms);
+    ++as_.n[k];
+    return e;
+  }
+  hipError_t t_malloc(void** p, size_t n) { return timed_call(0, [&] { return hipMalloc(p, n); }); }
+  hipError_t t_free(void* p) { return timed_call(1, [&] { return hipFree(p); }); }
+  hipError_t t_meminfo(size_t* f, size_t* t) { return timed_call(2, [&] { return hipMemGetInfo(f, t); }); }
   int device = 0, rank = 0, world = 1;
   hipStream_t stream = nullptr;
   std::unique_ptr<Collective> coll_;
@@ -2611,13 +2635,15 @@ struct DeviceCtx : Evaluator {
     ctx_count_add(device, 1);
   }
   ~DeviceCtx() override {
+    const auto td0 = std::chrono::steady_clock::now();
+    const AllocStats before = as_;
     ctx_count_add(device, -1);
     (void)hipSetDevice(device);
     coll_.reset();
     for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src, d_jade})
-      if (p) (void)hipFree(p);
-    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc})  // d_wsl lies inside d_wsc's allocation
-      if (p) (void)hipFree(p);
+      if (p) (void)t_free(p);
+    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc, (void*)d_xsf})  // d_wsl lies inside d_wsc's allocation
+      if (p) (void)t_free(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (auto& pr : ar_ev_)
       for (auto& e : pr)
@@ -2628,6 +2654,16 @@ struct DeviceCtx : Evaluator {
       if (sl->ev) (void)hipEventDestroy(sl->ev);
     }
     if (stream) (void)hipStreamDestroy(stream);
+    // the release as a whole: hipDeviceSynchronize charges any deferred work of the frees to
+    // this teardown instead of to the next context's first allocation
+    const auto ts = std::chrono::steady_clock::now();
+    (void)hipDeviceSynchronize();
+    const double sync_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+    std::lock_guard<std::mutex> lk(g_teardown_mu);
+    g_teardown[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td0).count();
+    g_teardown[1] = as_.ms[1] - before.ms[1];
+    g_teardown[2] = as_.mx[1];
+    g_teardown[3] = sync_ms;
   }
 
   uint64_t n_features() const override { return nf; }
@@ -2670,16 +2706,16 @@ struct DeviceCtx : Evaluator {
 
   double* ensure(double*& p, size_t& cap, size_t n) {
     if (n > cap) {
-      if (p) HIP_OK(hipFree(p));
+      if (p) HIP_OK(t_free(p));
       p = nullptr;
       cap = 0;
-      if (hipMalloc(&p, n * sizeof(double)) != hipSuccess) {
+      if (t_malloc((void**)&p, n * sizeof(double)) != hipSuccess) {
         (void)hipGetLastError();
         // the int8 slice image is a cache: its HBM goes to the pass buffers — unless the
         // ranks agreed on it (the screen branch issues its own collectives): then the
         // allocation fails instead and the group aborts rather than diverging
         if (!xsl_pinned()) release_xsl();
-        HIP_OK(hipMalloc(&p, n * sizeof(double)));
+        HIP_OK(t_malloc((void**)&p, n * sizeof(double)));
       }
       cap = n;
     }
@@ -2688,7 +2724,7 @@ struct DeviceCtx : Evaluator {
 
   void alloc_x(uint64_t nf_, uint64_t n_local, uint64_t n_tot, uint64_t t0_) {
     HIP_OK(hipSetDevice(device));
-    if (X) HIP_OK(hipFree(X));
+    if (X) HIP_OK(t_free(X));
     nf = nf_; n_local_ = n_local; n_total = n_tot; t0 = t0_;
     xshift_.clear();
     raw_sums_.clear();
@@ -2697,7 +2733,7 @@ struct DeviceCtx : Evaluator {
     wsl_nc_ = 0;    // … and W is sliced again (n_features may change)
     ldx = (n_local + 127) / 128 * 128;  // a fused-pass tile (≤ 128 samples) never crosses a row end
     if (ldx == 0) ldx = 128;
-    HIP_OK(hipMalloc(&X, nf * ldx * sizeof(double) + 256));
+    HIP_OK(t_malloc((void**)&X, nf * ldx * sizeof(double) + 256));
     HIP_OK(hipMemsetAsync(X, 0, nf * ldx * sizeof(double) + 256, stream));
   }
 
@@ -3428,7 +3464,7 @@ struct DeviceCtx : Evaluator {
     // has free next to X (at least 24 GB): C4 (256 × 1e7, 61 GB) is one chunk
     if (tiled_budget_ == 0) {
       size_t fr = 0, tot = 0;
-      HIP_OK(hipMemGetInfo(&fr, &tot));
+      HIP_OK(t_meminfo(&fr, &tot));
       const double have = (double)fr + (double)cap_tbuf * sizeof(double) - 16e9;
       tiled_budget_ = std::max(24e9, std::min(have, 0.6 * (double)tot));
     }
@@ -3484,9 +3520,9 @@ struct DeviceCtx : Evaluator {
     if (need <= cap_ybuf) return true;
     if (ybuf_failed) return false;
     size_t fr = 0, tot = 0;
-    HIP_OK(hipMemGetInfo(&fr, &tot));
-    if (d_ybuf) { HIP_OK(hipFree(d_ybuf)); fr += cap_ybuf * sizeof(double); d_ybuf = nullptr; cap_ybuf = 0; }
-    if (need * sizeof(double) + (size_t(2) << 30) > fr || hipMalloc(&d_ybuf, need * sizeof(double)) != hipSuccess) {
+    HIP_OK(t_meminfo(&fr, &tot));
+    if (d_ybuf) { HIP_OK(t_free(d_ybuf)); fr += cap_ybuf * sizeof(double); d_ybuf = nullptr; cap_ybuf = 0; }
+    if (need * sizeof(double) + (size_t(2) << 30) > fr || t_malloc((void**)&d_ybuf, need * sizeof(double)) != hipSuccess) {
       (void)hipGetLastError();
       d_ybuf = nullptr;
       ybuf_failed = true;
@@ -3513,10 +3549,37 @@ struct DeviceCtx : Evaluator {
   // free the slice image for good (until the next load / generate): the fp64 Y stage
   // serves every pass from then on
   void release_xsl() {
-    if (d_xsl) { HIP_OK(hipStreamSynchronize(stream)); (void)hipFree(d_xsl); (void)hipFree(d_xsc); }
+    if (d_xsl) { HIP_OK(hipStreamSynchronize(stream)); (void)t_free(d_xsl); (void)t_free(d_xsc); }
     d_xsl = nullptr; d_xsc = nullptr; cap_xsl = 0;
+    if (d_xsf) { (void)t_free(d_xsf); d_xsf = nullptr; }
+    cap_xsf_ = 0;
+    xsf_e0_ = INT_MIN;
     xsl_valid_ = false;
     xsl_failed_ = true;
+  }
+  // fp32 sample scales 2^(e_t − E0) of the digit image for k_screen_oz2 (screen.hip), built
+  // on first use per image (E0 = the image's largest exponent); xsf_e0_ = INT_MIN: not built
+  float* d_xsf = nullptr;
+  size_t cap_xsf_ = 0;
+  int xsf_e0_ = INT_MIN;
+  // false when the second screen cannot run here (the caller uses k_screen_oz)
+  bool ensure_xsf() {
+    if (!xsc_range_ok_ || xsc_emax_ - xsc_emin_ > 100) return false;  // u = y'·2^(e_t − E0) stays normal
+    if (xsf_e0_ == xsc_emax_ && d_xsf) return true;
+    if (cap_xsf_ < ldx) {
+      if (d_xsf) (void)t_free(d_xsf);
+      d_xsf = nullptr;
+      cap_xsf_ = 0;
+      if (t_malloc((void**)&d_xsf, ldx * sizeof(float)) != hipSuccess) {
+        (void)hipGetLastError();
+        d_xsf = nullptr;
+        return false;
+      }
+      cap_xsf_ = ldx;
+    }
+    HIP_OK(screen2_build_xsf(d_xsc, ldx, xsc_emax_, d_xsf, stream));
+    xsf_e0_ = xsc_emax_;
+    return true;
   }
   // the shapes the i8 loss kernel covers: 64 < nc ≤ 128, nf ≤ 128, centred X
   bool oz_shape(size_t nc) const { return y_stage_ != 1 && pick_nb(nc) == 8 && nf <= 128 && nf > 0; }
@@ -3538,20 +3601,21 @@ struct DeviceCtx : Evaluator {
     const size_t need = (size_t)n_blocks * oz_bb();
     if (need > cap_xsl) {
       size_t fr = 0, tot = 0;
-      HIP_OK(hipMemGetInfo(&fr, &tot));
-      if (d_xsl) { HIP_OK(hipFree(d_xsl)); HIP_OK(hipFree(d_xsc)); fr += cap_xsl + ldx * sizeof(double); }
+      HIP_OK(t_meminfo(&fr, &tot));
+      if (d_xsl) { HIP_OK(t_free(d_xsl)); HIP_OK(t_free(d_xsc)); fr += cap_xsl + ldx * sizeof(double); }
       d_xsl = nullptr; d_xsc = nullptr; cap_xsl = 0;
       // keep ≥ 4 GB free next to X for the pass buffers; otherwise stay on fp64
-      if (need + ldx * sizeof(double) + (size_t(4) << 30) > fr || hipMalloc(&d_xsl, need) != hipSuccess ||
-          hipMalloc(&d_xsc, ldx * sizeof(double)) != hipSuccess) {
+      if (need + ldx * sizeof(double) + (size_t(4) << 30) > fr || t_malloc((void**)&d_xsl, need) != hipSuccess ||
+          t_malloc((void**)&d_xsc, ldx * sizeof(double)) != hipSuccess) {
         (void)hipGetLastError();
-        if (d_xsl) (void)hipFree(d_xsl);
+        if (d_xsl) (void)t_free(d_xsl);
         d_xsl = nullptr; d_xsc = nullptr;
         xsl_failed_ = true;
         return false;
       }
       cap_xsl = need;
     }
+    xsf_e0_ = INT_MIN;  // the fp32 scales follow the image
     const unsigned grid = (unsigned)std::min<uint64_t>(n_blocks, (uint64_t)n_cu * 16);
     if (oz_kso() == 1) k_slice_x<1><<<grid, 64, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     else if (oz_kso() == 2) k_slice_x<2><<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
@@ -3608,7 +3672,7 @@ struct DeviceCtx : Evaluator {
   static constexpr size_t WSC_BYTES = 512 * sizeof(double);
   void alloc_wsl() {
     if (!d_wsc) {
-      HIP_OK(hipMalloc(&d_wsc, WSC_BYTES + WSL_IMG_MAX));
+      HIP_OK(t_malloc((void**)&d_wsc, WSC_BYTES + WSL_IMG_MAX));
       d_wsl = (uint8_t*)d_wsc + WSC_BYTES;
     }
   }
@@ -3881,8 +3945,43 @@ struct DeviceCtx : Evaluator {
     ++n_int8_passes_;
     ++n_screen_passes_;
   }
+  // k_screen_oz2 (screen.hip): the same statistics and bound as k_screen_oz on the interleaved
+  // schedule; PICARD_SCREEN_V2=0 keeps k_screen_oz. false: not available here.
+  bool screen_v2_ = !(std::getenv("PICARD_SCREEN_V2") && std::atoi(std::getenv("PICARD_SCREEN_V2")) == 0);
+  template <int NB>
+  bool launch_screen_oz2(double alpha, double* st_rows) {
+    constexpr int NCP = 16 * NB;
+    const int U = screen2_blocks_per_step(NB);
+    const uint64_t n_blocks = (n_local_ + 15) / 16;
+    const uint64_t want = std::min<uint64_t>((uint64_t)2 * n_cu, std::max<uint64_t>((n_blocks + U - 1) / U, 1));
+    const uint64_t steps_per_wg = ((n_blocks + U - 1) / U + want - 1) / want;
+    const uint64_t bpw = steps_per_wg * U;
+    const int nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
+    // 32-bit buffer offsets within a workgroup's range (and the kernel's 32-bit block counts)
+    if ((bpw + 2 * (uint64_t)U) * screen2_tile_bytes(NB) >= (1ull << 31) || n_blocks >= (1ull << 32)) return false;
+    if (!ensure_xsf()) return false;
+    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
+    if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
+    if (oz_kso() != (NB == 8 ? 2 : 1)) throw computation_error("int8 digit image of another layout");
+    Screen2Args a;
+    a.xsl = d_xsl; a.xsf = d_xsf; a.wsl = d_wsl; a.wsc = d_wsc;
+    a.c32 = (float)(-2.0 * alpha * fm::LOG2E);
+    a.e0 = xsf_e0_;
+    a.ln2_alpha = fm::LN2 / alpha;
+    a.bpw = (uint32_t)bpw; a.n_blocks = (uint32_t)n_blocks; a.nwg = nwg; a.partials = part;
+    HIP_OK(hipEventRecord(ev[1], stream));
+    HIP_OK(screen2_launch(NB, a, stream));
+    HIP_OK(hipEventRecord(ev[2], stream));
+    k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
+        part, nwg, 2 * NCP, 0, NCP, (int)kept_nc_pending, 2, st_rows, DENS_TANH, alpha, (double)n_local_, 1);
+    HIP_OK(hipGetLastError());
+    ++n_int8_passes_;
+    ++n_screen_passes_;
+    return true;
+  }
   template <int NB>
   void screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
+    if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && launch_screen_oz2<NB>(d.alpha, st_rows)) return;
     if (f32l && dmax == 3 && screen_nows_) launch_screen_oz<3, NB>(d.alpha, st_rows);
     else if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);
     else if (f32l) launch_loss_oz<DENS_TANH, false, 4, true, NB>(d.alpha, false, st_rows);
@@ -4417,6 +4516,20 @@ void device_ctx_comm_stats(const Evaluator* e, int64_t* out) {
   out[4] = d->coll_ && d->coll_->aborted() ? 1 : 0;
   out[5] = d->world;
   out[6] = !d->coll_ ? 0 : std::strcmp(d->coll_->kind(), "rccl") == 0 ? 1 : 2;
+}
+// [0..2] ms in hipMalloc / hipFree / hipMemGetInfo, [3..5] their counts, [6..8] the largest
+// single call of each
+void device_ctx_alloc_stats(const Evaluator* e, double* out) {
+  auto* d = static_cast<const DeviceCtx*>(e);
+  for (int k = 0; k < 3; ++k) {
+    out[k] = d->as_.ms[k];
+    out[3 + k] = (double)d->as_.n[k];
+    out[6 + k] = d->as_.mx[k];
+  }
+}
+void device_last_teardown(double* out) {
+  std::lock_guard<std::mutex> lk(g_teardown_mu);
+  for (int k = 0; k < 4; ++k) out[k] = g_teardown[k];
 }
 // [0] ms inside all-reduces (see DeviceCtx::allreduce), [1] all-reduces timed
 void device_ctx_comm_timing(const Evaluator* e, double* out) {

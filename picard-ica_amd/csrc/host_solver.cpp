@@ -246,6 +246,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   split_first_ = std::getenv("PICARD_SPLIT_FIRST") != nullptr;
   init_core();
   lap(4);
+  for (int i = 0; i < 5; ++i) setup_ms_[i] = tsm[i];
   if (trace_)
     std::fprintf(stderr, "[picard-trace] setup ms (cumulative): rowsum %.3f gram %.3f eigh %.3f w_init %.3f initial pass %.3f\n",
                  tsm[0], tsm[1], tsm[2], tsm[3], tsm[4]);

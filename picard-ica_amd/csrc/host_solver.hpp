@@ -56,6 +56,11 @@ class Solver {
   void last_timing(double out[4]) const {
     for (int i = 0; i < 4; ++i) out[i] = last_timing_[i];
   }
+  // setup phases, ms since the constructor started (cumulative): rowsum, Gram, eigh, w_init
+  // and warm start, initial pass (0 for a phase that did not run)
+  void setup_timing(double out[5]) const {
+    for (int i = 0; i < 5; ++i) out[i] = setup_ms_[i];
+  }
   uint64_t total_evals() const { return total_evals_; }
   uint64_t total_completions() const { return total_completions_; }
   uint64_t screen_passes() const { return screen_passes_; }
@@ -107,6 +112,7 @@ class Solver {
   bool converged_ = false, done_ = false;
   uint64_t last_evals_ = 0, total_evals_ = 0;
   double last_timing_[4] = {0.0, 0.0, 0.0, 0.0};
+  double setup_ms_[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   uint64_t total_completions_ = 0;
   uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
   bool screen_ok_ = true;  // false once the evaluator declined a screen (then never asked again)

@@ -1,0 +1,261 @@
+// The orthogonal line-search screen, second form (k_screen_oz2): the same bound as
+// k_screen_oz (ozaki.inc) — diagonals D ≤ 3 of the exact int8 digit stage, the fp32 combine
+// and fp32 ℓ with the error terms DeviceCtx::screen_at adds — on a schedule built from the
+// issue costs measured on MI355X (tools/microbench/fill_coexec.hip, profiles/r04_a):
+//
+//   * an i8 MFMA (v_mfma_i32_16x16x64_i8) holds its SIMD's vector issue for ≈ 12 of its 16
+//     cycles, and vector instructions co-issue beside it only from the SAME wave (an MFMA wave
+//     beside a VALU wave runs serialised: tools/microbench/agpr_coexec.hip). So each wave
+//     interleaves the row terms of its previous step between the MFMAs of its current step
+//     (sched_group_barrier: one MFMA, then two vector instructions), instead of 20 MFMAs
+//     followed by a block of VALU;
+//   * fewer vector instructions per element: the sample scale 2^(e_t − E0) comes in fp32 from
+//     a per-image array (k_build_xsf, 4 B per sample, laid out so one ds_read_b128 gives a
+//     lane its 4 samples) and the row scale 2^(f_i + E0 − 20) is folded into the exp argument
+//     and the final row sums — both powers of two, so every rounding is the old kernel's;
+//   * the LDS-DMA staging is raw buffer loads (one 1-KiB piece per wave and step, the step
+//     offset in the lane offset: no 64-bit address arithmetic in the loop), and a piece past
+//     the workgroup's last block reads zeros (buffer range check): a zero digit block gives
+//     y = 0 exactly, whose row terms vanish (|0| = 0, 2^0 = 1, log2 1 = 0), so the loop needs
+//     no per-step bounds tests;
+//   * 8 waves per workgroup, two workgroups per CU (the two barrier streams interleave).
+//
+// Not a standalone translation unit for the library's host code: device.hip calls
+// screen2_launch / screen2_build_xsf through the declarations in screen2.hpp.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "screen2.hpp"
+
+namespace pcamd {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int SLICES = 7;  // digits per value (ozaki.inc OZ_SLICES)
+constexpr int RSRC_DW3 = 0x00020000;  // raw buffer descriptor word 3 (gfx9 family)
+
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (void*)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ v4i mfma_i8(v4i a, v4i b, v4i c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// One step's row terms of a lane (4 samples lk + 4r of row lr): the D ≤ 3 diagonal sums
+// acc[0..3] → y' = fl(fl(R23)·2^-16 + fl(Q01)) (oz_combine_screen_f32's arithmetic), u = y'·sf
+// (sf = 2^(e_t − E0), exact), z = fl(|u|·cz) (cz = |c32|·2^(f_i + E0 − 20): the same fl(|ỹ|·c32)
+// as loss_acc4_f32y, negated), then Σ|u| in fp32 ((|u0| + |u1|) + (|u2| + |u3|)) into l and
+// log2 Π (1 + 2^−z)/2 into g — every rounding of loss_acc4_f32y's per-element arithmetic, on
+// values scaled by exact powers of two.
+__device__ __forceinline__ void row_terms(const v4i (&acc)[4], const f4v& sf, float cz, double& l, double& g) {
+  float u[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q01 = acc[0][r] * 256 + acc[1][r], r23 = acc[2][r] * 256 + acc[3][r];
+    u[r] = __builtin_fmaf((float)r23, 0x1p-16f, (float)q01) * sf[r];
+  }
+  float f[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) f[r] = __builtin_fmaf(__builtin_amdgcn_exp2f(-(__builtin_fabsf(u[r]) * cz)), 0.5f, 0.5f);
+  const float s = (__builtin_fabsf(u[0]) + __builtin_fabsf(u[1])) + (__builtin_fabsf(u[2]) + __builtin_fabsf(u[3]));
+  l += (double)s;
+  g += (double)__builtin_amdgcn_logf((f[0] * f[1]) * (f[2] * f[3]));
+}
+
+template <int NB>
+struct S2 {
+  static constexpr int KSO = NB == 8 ? 2 : 1;          // k-steps of 64 features
+  static constexpr int U = 8 / NB;                     // 16-sample blocks per step
+  static constexpr int NCP = 16 * NB;                  // rows of the partials
+  static constexpr int TILE = SLICES * KSO * 1024;     // bytes of one block's digit image
+  static constexpr int PL = 4;                         // digit planes the screen reads (D ≤ 3)
+  static constexpr int SLOT = PL * KSO * 1024;         // LDS bytes of one block's planes
+  static constexpr int PIECES = PL * KSO;              // 1-KiB pieces per block (U·PIECES = 8)
+  static constexpr int NBUF = 3, SCB = 256;
+  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + U * NCP * 2 * 8;
+};
+
+template <int NB>
+__global__ void __launch_bounds__(512, 2)
+k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
+             const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
+             double* __restrict__ partials) {
+  using S = S2<NB>;
+  constexpr int KSO = S::KSO, U = S::U, NCP = S::NCP, TILE = S::TILE, SLOT = S::SLOT, NBUF = S::NBUF;
+  static_assert(U * S::PIECES == 8, "one piece per wave and step");
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int lr = lane & 15, lk = lane >> 4;
+  const int yi = wv % NB, h = wv / NB;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tiles = smem;                            // [NBUF][U][SLOT]
+  uint8_t* scl = tiles + NBUF * U * SLOT;           // [NBUF][SCB]: U·16 fp32 scales (+ DMA overhang)
+  double* red = (double*)(scl + NBUF * S::SCB);     // [U][NCP][2]
+  const uint32_t b_begin = blockIdx.x * bpw;
+  const uint32_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint32_t nb = b_begin < b_end ? b_end - b_begin : 0u;
+  const uint32_t nsteps = (nb + U - 1) / U;
+  // buffer resources over this workgroup's blocks only: a piece past its last block reads 0
+  // (the operands are wave-uniform; readfirstlane keeps the descriptors in SGPRs, else every
+  // buffer load becomes a waterfall loop)
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(xsl + (size_t)b_begin * TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * TILE)), RSRC_DW3);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
+  // this wave's piece of every step: block bp of the step, piece q (planes 0–3 are the first
+  // PL·KSO KiB of a block image); wave 7 also moves the step's U·16 scales (lanes repeat)
+  const int bp = wv / S::PIECES, q = wv % S::PIECES;
+  const uint32_t voff_x = (uint32_t)(bp * TILE + q * 1024 + lane * 16);
+  const uint32_t voff_s = (uint32_t)((lane & (16 * U - 1)) * 4);
+  const bool scale_wave = wv == 7;
+  auto stage = [&](uint32_t step, int buf) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bp) * SLOT + q * 1024), 16,
+                                             (int)(voff_x + step * (uint32_t)(U * TILE)), 0, 0, 0);
+    if (scale_wave)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB), 4,
+                                               (int)(voff_s + step * (uint32_t)(U * 64)), 0, 0, 0);
+  };
+  // end of a step: this wave's piece(s) of the NEXT step landed (the ones just issued for the
+  // step after may still fly: counted vmcnt), then every wave meets
+  // (lgkmcnt(0): this step's scale read has returned before the next step's DMA may overwrite
+  // its buffer)
+  auto step_barrier = [&]() {
+    if (scale_wave) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  v4i wsl[4][KSO];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int s = 0; s < KSO; ++s)
+      wsl[a][s] = *(const v4i*)(wsl_g + (size_t)(((yi * SLICES + a) * 2 + s) * 64 + lane) * 16);
+  const double rowscale = __builtin_ldexp(wsc[yi * 16 + lr], e0 - 8);  // 2^(f_i + E0 − 20)
+  const float cz = __builtin_fabsf(c32) * (float)rowscale;               // exact: a power-of-2 scaling
+  double l = 0.0, g = 0.0;
+  v4i acc[2][4];
+  f4v sf[2];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[1][d] = v4i{0, 0, 0, 0};  // the "previous step" of step 0: zero terms
+  sf[1] = f4v{0.f, 0.f, 0.f, 0.f};
+  stage(0, 0);
+  stage(1, 1);
+  if (scale_wave) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // step k: stage k + 2; the MFMAs of step k with the row terms of step k − 1 between them
+  auto body = [&](uint32_t k, int buf, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value, prv = cur ^ 1;
+    stage(k + 2, buf == 0 ? 2 : buf - 1);  // (k + 2) mod 3; past the end: zeros, never read
+    const uint8_t* tile = tiles + (buf * U + h) * SLOT + lane * 16;
+    v4i xa[2][KSO];
+#pragma unroll
+    for (int s = 0; s < KSO; ++s) xa[0][s] = *(const v4i*)(tile + s * 1024);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (b < 3)
+#pragma unroll
+        for (int s = 0; s < KSO; ++s) xa[(b + 1) & 1][s] = *(const v4i*)(tile + ((b + 1) * KSO + s) * 1024);
+#pragma unroll
+      for (int s = 0; s < KSO; ++s)
+#pragma unroll
+        for (int a = 0; a <= 3 - b; ++a) {
+          const int d = a + b;
+          acc[cur][d] = (b == 0 && s == 0) ? mfma_i8(xa[b & 1][s], wsl[a][s], v4i{0, 0, 0, 0})
+                                           : mfma_i8(xa[b & 1][s], wsl[a][s], acc[cur][d]);
+        }
+    }
+    row_terms(acc[prv], sf[prv], cz, l, g);
+    sf[cur] = *(const f4v*)(scl + buf * S::SCB + h * 64 + lk * 16);
+    // one MFMA, then two vector instructions, over the 10·KSO MFMAs of the step
+#pragma unroll
+    for (int i = 0; i < 10 * KSO; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    }
+    // the row sums are complete here: keeps the row terms in this block (between the MFMAs)
+    // instead of sunk past the barrier's wait
+    asm volatile("" ::"v"(l), "v"(g));
+    step_barrier();
+  };
+  uint32_t k = 0;
+  int buf = 0;
+  for (; k + 1 < nsteps; k += 2) {
+    body(k, buf, std::integral_constant<int, 0>{});
+    buf = buf == 2 ? 0 : buf + 1;
+    body(k + 1, buf, std::integral_constant<int, 1>{});
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  if (k < nsteps) {
+    body(k, buf, std::integral_constant<int, 0>{});
+    row_terms(acc[0], sf[0], cz, l, g);
+  } else {
+    row_terms(acc[1], sf[1], cz, l, g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero pieces past the end: drained
+  double rs_y = l * rowscale;                       // Σ|ỹ| (exact scaling)
+  double rs_ll = __builtin_fma(g, ln2_alpha, rs_y);
+  rs_ll += __shfl_xor(rs_ll, 16); rs_ll += __shfl_xor(rs_ll, 32);
+  rs_y += __shfl_xor(rs_y, 16);   rs_y += __shfl_xor(rs_y, 32);
+  if (lk == 0) {
+    red[(h * NCP + yi * 16 + lr) * 2 + 0] = rs_ll;
+    red[(h * NCP + yi * 16 + lr) * 2 + 1] = rs_y;
+  }
+  __syncthreads();
+  double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
+  for (int e = threadIdx.x; e < 2 * NCP; e += 512) {
+    const int c = e / NCP, row = e % NCP;
+    double v = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) v += red[(u * NCP + row) * 2 + c];
+    out[e] = v;
+  }
+}
+
+// xsf[16·blk + 4·lk + r] = 2^(e_t − E0) in fp32 for sample t = 16·blk + lk + 4r (the lane's 4
+// samples of k_screen_oz2 contiguous): exact for the image's exponent range (host-checked)
+__global__ void __launch_bounds__(256) k_build_xsf(const double* __restrict__ xsc, uint64_t n, int e0,
+                                                   float* __restrict__ xsf) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t blk = i >> 4;
+    const int lk = (int)(i >> 2) & 3, r = (int)i & 3;
+    xsf[i] = (float)__builtin_ldexp(xsc[blk * 16 + lk + 4 * r], -e0);
+  }
+}
+
+template <int NB>
+hipError_t launch(const Screen2Args& a, hipStream_t stream) {
+  using S = S2<NB>;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  k_screen_oz2<NB><<<a.nwg, 512, S::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
+                                                    a.n_blocks, a.partials);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int screen2_blocks_per_step(int nb) { return 8 / nb; }
+uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }
+
+hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream) {
+  return nb == 8 ? launch<8>(a, stream) : launch<4>(a, stream);
+}
+
+hipError_t screen2_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream) {
+  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  k_build_xsf<<<grid ? grid : 1, 256, 0, stream>>>(xsc, n, e0, xsf);
+  return hipGetLastError();
+}
+
+}  // namespace pcamd
