@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "screen2.hpp"
 
@@ -80,7 +81,8 @@ struct S2 {
   static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + U * NCP * 2 * 8;
 };
 
-template <int NB>
+// FILL: vector instructions scheduled after each MFMA (0: no schedule groups, the compiler's order)
+template <int NB, int FILL>
 __global__ void __launch_bounds__(512, 2)
 k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
              const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
@@ -172,11 +174,13 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
     }
     row_terms(acc[prv], sf[prv], cz, l, g);
     sf[cur] = *(const f4v*)(scl + buf * S::SCB + h * 64 + lk * 16);
-    // one MFMA, then two vector instructions, over the 10·KSO MFMAs of the step
+    // one MFMA, then FILL vector instructions, over the 10·KSO MFMAs of the step
+    if constexpr (FILL > 0) {
 #pragma unroll
-    for (int i = 0; i < 10 * KSO; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      for (int i = 0; i < 10 * KSO; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, FILL, 0);
+      }
     }
     // the row sums are complete here: keeps the row terms in this block (between the MFMAs)
     // instead of sunk past the barrier's wait
@@ -228,24 +232,332 @@ __global__ void __launch_bounds__(256) k_build_xsf(const double* __restrict__ xs
   }
 }
 
-template <int NB>
-hipError_t launch(const Screen2Args& a, hipStream_t stream) {
+template <int NB, int FILL>
+hipError_t launch_fill(const Screen2Args& a, hipStream_t stream) {
   using S = S2<NB>;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB>,
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB, FILL>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_screen_oz2<NB><<<a.nwg, 512, S::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
-                                                    a.n_blocks, a.partials);
+  k_screen_oz2<NB, FILL><<<a.nwg, 512, S::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
+                                                          a.n_blocks, a.partials);
   return hipGetLastError();
 }
+// PICARD_SCREEN2_FILL (measurement knob): vector instructions per MFMA gap, 0 = compiler order
+int fill_knob() {
+  static const int v = [] {
+    const char* e = std::getenv("PICARD_SCREEN2_FILL");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+template <int NB>
+hipError_t launch(const Screen2Args& a, hipStream_t stream) {
+  switch (fill_knob()) {
+    case 0: return launch_fill<NB, 0>(a, stream);
+    case 1: return launch_fill<NB, 1>(a, stream);
+    case 3: return launch_fill<NB, 3>(a, stream);
+    default: return launch_fill<NB, 2>(a, stream);
+  }
+}
 
+
+// ---------------------------------------------------------------------------------------------
+// k_screen_oz3 (NB = 8: 64 < nc ≤ 128, nf ≤ 128): the same screen on v_mfma_i32_32x32x32_i8.
+// That MFMA runs 32 cycles for the MACs of two 16x16x64 but holds its wave's vector issue for
+// only ≈ 8–10 of them (tools/microbench/fill_coexec.hip, profiles/r04_a: 4 fp32 FMAs ride along
+// in 34 cycles), so the row terms of the previous step fit in the gaps of the current step's
+// MFMAs and the kernel runs at the matrix pipe instead of at the issue port.
+//
+// Operands (no new X image): the 32x32x32 A operand of 32 samples × 32 features is read from the
+// 16x16x64 digit image of two blocks — lane l takes the 16 bytes of image lane
+// (l mod 16) + 16·(2c + l/32) of block (l mod 32)/16 (chunk c of the k-step) — and the B operand
+// (W) is gathered from the W digit image with the same feature ↔ (lane group, byte) map, so both
+// operands agree on every feature whatever order the instruction sums them in. Output (32 × 32
+// i32, 16 registers): lane l holds W row 32·rt + (l mod 32) and the 16 samples-rows
+// m = 8(r/4) + 4(l/32) + (r mod 4) of the pair, i.e. block m/16 of the pair, image row m mod 16
+// (sample σ(m mod 16) = ((m mod 16) >> 2) + 4((m mod 16) & 3), ozaki.inc).
+// Per element the arithmetic of row_terms (so the same bound); the Σ|u| partial sums group 4
+// samples as there, each 4-sample product of (1 + 2^−z)/2 gets one log.
+// 8 waves, one workgroup per CU (≈ 230 VGPRs per wave): wave w takes row tile rt = w & 3 and pair
+// pp = w >> 2 of every step (4 blocks, 64 samples).
+// ---------------------------------------------------------------------------------------------
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ v16i mfma32_i8(v4i a, v4i b, v16i c) {
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+
+struct S3 {
+  static constexpr int KSO = 2, U = 4, NCP = 128, TILE = SLICES * KSO * 1024;
+  static constexpr int SLOT = 4 * KSO * 1024, NBUF = 3, SCB = 256;
+  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + 2 * NCP * 2 * 8;
+};
+
+// 16 row terms of a lane: q01 = P0·256 + P1, r23 = P2·256 + P3 (int32, exact) of samples r,
+// scales sf[r] = 2^(e_t − E0)
+__device__ __forceinline__ void row_terms16(const v16i& q01, const v16i& r23, const float (&sf)[16], float cz,
+                                            double& l, double& g) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float u[4], f[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * q + i;
+      u[i] = __builtin_fmaf((float)r23[r], 0x1p-16f, (float)q01[r]) * sf[r];
+      f[i] = __builtin_fmaf(__builtin_amdgcn_exp2f(-(__builtin_fabsf(u[i]) * cz)), 0.5f, 0.5f);
+    }
+    l += (double)((__builtin_fabsf(u[0]) + __builtin_fabsf(u[1])) + (__builtin_fabsf(u[2]) + __builtin_fabsf(u[3])));
+    g += (double)__builtin_amdgcn_logf((f[0] * f[1]) * (f[2] * f[3]));
+  }
+}
+
+// The row terms of the previous step cut into 40 slots, one after each MFMA of the current step
+// (k_screen_oz3): slots 0–15 combine element r = slot (y' = fl(fl(R23)·2^-16 + fl(Q01)), u = y'·sf),
+// 16–31 its ℓ factor ((1 + 2^−|u|·cz)/2), 32–39 the two halves of each 4-element group's end
+// (the product and its log; Σ|u| and both fp64 accumulations) — row_terms' arithmetic, element
+// for element.
+struct RT3 {
+  float u[16], f[16];
+  float lg[4];
+};
+template <int J>
+__device__ __forceinline__ void rt_slot(RT3& t, const v16i& q01, const v16i& r23, const float (&sf)[16], float cz,
+                                        double& l, double& g) {
+  if constexpr (J < 16) {
+    t.u[J] = __builtin_fmaf((float)r23[J], 0x1p-16f, (float)q01[J]) * sf[J];
+  } else if constexpr (J < 32) {
+    constexpr int r = J - 16;
+    t.f[r] = __builtin_fmaf(__builtin_amdgcn_exp2f(-(__builtin_fabsf(t.u[r]) * cz)), 0.5f, 0.5f);
+  } else if constexpr ((J & 1) == 0) {
+    constexpr int q = (J - 32) >> 1;
+    t.lg[q] = __builtin_amdgcn_logf((t.f[4 * q] * t.f[4 * q + 1]) * (t.f[4 * q + 2] * t.f[4 * q + 3]));
+  } else {
+    constexpr int q = (J - 32) >> 1;
+    l += (double)((__builtin_fabsf(t.u[4 * q]) + __builtin_fabsf(t.u[4 * q + 1])) +
+                  (__builtin_fabsf(t.u[4 * q + 2]) + __builtin_fabsf(t.u[4 * q + 3])));
+    g += (double)t.lg[q];
+  }
+}
+
+// schedule groups of k_screen_oz3: MFMA i, then the vector instructions of its slot
+template <int I>
+struct Oz3Groups {
+  static constexpr int NV = (I < 16 ? 4 : I < 32 ? 3 : (I & 1) == 0 ? 4 : 7) + (I >= 12 && I < 28 ? 1 : 0);
+  static __device__ __forceinline__ void emit() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    Oz3Groups<I + 1>::emit();
+  }
+};
+template <>
+struct Oz3Groups<40> {
+  static __device__ __forceinline__ void emit() {}
+};
+
+template <int FILL>
+__global__ void __launch_bounds__(512, 1)
+k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
+             const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
+             double* __restrict__ partials) {
+  using S = S3;
+  constexpr int U = S::U, TILE = S::TILE, SLOT = S::SLOT, NCP = S::NCP;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int rt = wv & 3, pp = wv >> 2;
+  const int n = lane & 31, gl = lane >> 5;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tiles = smem;                         // [NBUF][U][SLOT]
+  uint8_t* scl = tiles + S::NBUF * U * SLOT;     // [NBUF][SCB]: 2 pairs × [2][16] fp32 scales
+  double* red = (double*)(scl + S::NBUF * S::SCB);  // [2][NCP][2]
+  const uint32_t b_begin = blockIdx.x * bpw;
+  const uint32_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint32_t nb = b_begin < b_end ? b_end - b_begin : 0u;
+  const uint32_t nsteps = (nb + U - 1) / U;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(xsl + (size_t)b_begin * TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * TILE)), RSRC_DW3);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
+  // DMA: wave w moves pieces 4(w & 1) … 4(w & 1) + 3 (1 KiB each) of block w >> 1 of the step;
+  // wave 7 also the step's 64 scales (one dword per lane)
+  const int bq = wv >> 1, p0 = 4 * (wv & 1);
+  const uint32_t voff_x = (uint32_t)(bq * TILE + p0 * 1024 + lane * 16);
+  const bool scale_wave = wv == 7;
+  auto stage = [&](uint32_t step, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bq) * SLOT + (p0 + i) * 1024), 16,
+                                               (int)(voff_x + i * 1024 + step * (uint32_t)(U * TILE)), 0, 0, 0);
+    if (scale_wave)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB), 4,
+                                               (int)(lane * 4 + step * (uint32_t)(U * 64)), 0, 0, 0);
+  };
+  // B operands: W rows 32rt + n, digits a ≤ 3, k-step s, chunk c: the 16 bytes of W-image lane
+  // (n mod 16) + 16(2c + gl) of row block 2rt + n/16 (the A operand's feature map)
+  v4i wb[4][2][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        wb[a][s][c] = *(const v4i*)(wsl_g + (size_t)((((2 * rt + (n >> 4)) * SLICES + a) * 2 + s) * 64 + (n & 15) +
+                                                     16 * (2 * c + gl)) * 16);
+  const double rowscale = __builtin_ldexp(wsc[rt * 32 + n], e0 - 8);  // 2^(f_i + E0 − 20)
+  const float cz = __builtin_fabsf(c32) * (float)rowscale;
+  // A operand of plane b, k-step s, chunk c in a staged pair: block (n >> 4) of the pair,
+  // image lane (n & 15) + 16(2c + gl)
+  const uint32_t a_lane = (uint32_t)((n >> 4) * SLOT + ((n & 15) + 16 * gl) * 16);
+  double l = 0.0, g = 0.0;
+  v16i q01p, r23p;  // the previous step's merged diagonals (zero before step 0: zero terms)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) q01p[r] = r23p[r] = 0;
+  float sfp[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) sfp[r] = 0.f;
+  stage(0, 0);
+  stage(1, 1);
+  if (scale_wave) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint32_t k = 0;
+  int buf = 0;
+  for (; k < nsteps; ++k) {
+    stage(k + 2, buf == 0 ? 2 : buf - 1);  // (k + 2) mod 3; past the end: zeros, never read
+    const uint8_t* pb = tiles + (buf * U + 2 * pp) * SLOT + a_lane;
+    auto ra = [&](int b, int s, int c) { return *(const v4i*)(pb + ((b * 2 + s) * 64 + 32 * c) * 16); };
+    v16i acc[4];
+    RT3 t;
+    int j = 0;  // MFMA index of the step: its row-term slot follows it
+    auto after = [&](auto jc) {
+      constexpr int J = decltype(jc)::value;
+      if constexpr (FILL > 0) rt_slot<J>(t, q01p, r23p, sfp, cz, l, g);
+    };
+    (void)j;
+    // phase 1: D ≤ 1 (12 MFMAs: slots 0–11)
+#define OZ3_P1(S_, C_, J0)                                                                       \
+    {                                                                                            \
+      const v4i x0 = ra(0, S_, C_), x1 = ra(1, S_, C_);                                          \
+      acc[0] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[0][S_][C_], v16i{}) : mfma32_i8(x0, wb[0][S_][C_], acc[0]); \
+      after(std::integral_constant<int, J0>{});                                                  \
+      acc[1] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[1][S_][C_], v16i{}) : mfma32_i8(x0, wb[1][S_][C_], acc[1]); \
+      after(std::integral_constant<int, J0 + 1>{});                                              \
+      acc[1] = mfma32_i8(x1, wb[0][S_][C_], acc[1]);                                             \
+      after(std::integral_constant<int, J0 + 2>{});                                              \
+    }
+    OZ3_P1(0, 0, 0) OZ3_P1(0, 1, 3) OZ3_P1(1, 0, 6) OZ3_P1(1, 1, 9)
+#undef OZ3_P1
+    v16i q01;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) q01[r] = acc[0][r] * 256 + acc[1][r];
+    // phase 2: D = 2, 3 (28 MFMAs: slots 12–39)
+#define OZ3_P2(S_, C_, J0)                                                                       \
+    {                                                                                            \
+      const v4i x0 = ra(0, S_, C_), x1 = ra(1, S_, C_), x2 = ra(2, S_, C_), x3 = ra(3, S_, C_);  \
+      acc[2] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[2][S_][C_], v16i{}) : mfma32_i8(x0, wb[2][S_][C_], acc[2]); \
+      after(std::integral_constant<int, J0>{});                                                  \
+      acc[3] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[3][S_][C_], v16i{}) : mfma32_i8(x0, wb[3][S_][C_], acc[3]); \
+      after(std::integral_constant<int, J0 + 1>{});                                              \
+      acc[2] = mfma32_i8(x1, wb[1][S_][C_], acc[2]);                                             \
+      after(std::integral_constant<int, J0 + 2>{});                                              \
+      acc[3] = mfma32_i8(x1, wb[2][S_][C_], acc[3]);                                             \
+      after(std::integral_constant<int, J0 + 3>{});                                              \
+      acc[2] = mfma32_i8(x2, wb[0][S_][C_], acc[2]);                                             \
+      after(std::integral_constant<int, J0 + 4>{});                                              \
+      acc[3] = mfma32_i8(x2, wb[1][S_][C_], acc[3]);                                             \
+      after(std::integral_constant<int, J0 + 5>{});                                              \
+      acc[3] = mfma32_i8(x3, wb[0][S_][C_], acc[3]);                                             \
+      after(std::integral_constant<int, J0 + 6>{});                                              \
+    }
+    OZ3_P2(0, 0, 12) OZ3_P2(0, 1, 19) OZ3_P2(1, 0, 26) OZ3_P2(1, 1, 33)
+#undef OZ3_P2
+    if constexpr (FILL == 0) row_terms16(q01p, r23p, sfp, cz, l, g);
+    if constexpr (FILL > 0) {
+      // the schedule: each MFMA, then its slot's vector instructions (slot sizes as lowered:
+      // 4 = 2 cvt + fma + mul; 3 = mul + exp + fma; 4 = 3 mul + log; 7 = 3 add + 2 cvt + 2 add_f64),
+      // the 16 q01 merges spread over slots 12–27
+      Oz3Groups<0>::emit();
+    }
+    asm volatile("" ::"v"(l), "v"(g));  // the row terms stay in this block (not sunk past the wait)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) r23p[r] = acc[2][r] * 256 + acc[3][r];
+    q01p = q01;
+    // this step's scales: pair pp, lane group gl — 16 floats (the layout of k_build_xsf3)
+    {
+      const float* sp = (const float*)(scl + buf * S::SCB) + pp * 32 + gl * 16;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const f4v tv = *(const f4v*)(sp + 4 * v);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sfp[4 * v + i] = tv[i];
+      }
+    }
+    if (scale_wave) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  row_terms16(q01p, r23p, sfp, cz, l, g);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  double rs_y = l * rowscale;
+  double rs_ll = __builtin_fma(g, ln2_alpha, rs_y);
+  rs_ll += __shfl_xor(rs_ll, 32);
+  rs_y += __shfl_xor(rs_y, 32);
+  if (gl == 0) {
+    red[(pp * NCP + rt * 32 + n) * 2 + 0] = rs_ll;
+    red[(pp * NCP + rt * 32 + n) * 2 + 1] = rs_y;
+  }
+  __syncthreads();
+  double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
+  for (int e = threadIdx.x; e < 2 * NCP; e += 512) {
+    const int c = e / NCP, row = e % NCP;
+    out[e] = red[row * 2 + c] + red[(NCP + row) * 2 + c];
+  }
+}
+
+// xsf3[32·p + 16·gl + r] = 2^(e_t − E0) for the sample of output row m = 8(r/4) + 4gl + (r mod 4)
+// of block pair p: block 2p + m/16, image row m mod 16, sample σ(m mod 16) (k_screen_oz3's map)
+__global__ void __launch_bounds__(256) k_build_xsf3(const double* __restrict__ xsc, uint64_t n, int e0,
+                                                    float* __restrict__ xsf) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t p = i >> 5;
+    const int gl = (int)(i >> 4) & 1, r = (int)i & 15;
+    const int m = 8 * (r >> 2) + 4 * gl + (r & 3);
+    const int m16 = m & 15, sig = (m16 >> 2) + 4 * (m16 & 3);
+    xsf[i] = (float)__builtin_ldexp(xsc[(2 * p + (m >> 4)) * 16 + sig], -e0);
+  }
+}
+
+template <int FILL>
+hipError_t launch3_fill(const Screen2Args& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz3<FILL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             S3::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  k_screen_oz3<FILL><<<a.nwg, 512, S3::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
+                                                       a.n_blocks, a.partials);
+  return hipGetLastError();
+}
+hipError_t launch3(const Screen2Args& a, hipStream_t stream) {
+  // PICARD_SCREEN2_FILL=0: the row terms in the compiler's order; otherwise one slot per MFMA
+  return fill_knob() == 0 ? launch3_fill<0>(a, stream) : launch3_fill<1>(a, stream);
+}
 }  // namespace
 
 int screen2_blocks_per_step(int nb) { return 8 / nb; }
+int screen3_blocks_per_step() { return S3::U; }
+hipError_t screen3_launch(const Screen2Args& a, hipStream_t stream) { return launch3(a, stream); }
+hipError_t screen3_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream) {
+  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  k_build_xsf3<<<grid ? grid : 1, 256, 0, stream>>>(xsc, n, e0, xsf);
+  return hipGetLastError();
+}
 uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }
 
 hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream) {
