@@ -3986,21 +3986,22 @@ struct DeviceCtx : Evaluator {
     ++n_screen_passes_;
     return true;
   }
-  // k_screen_oz3 (NB = 8, v_mfma_i32_32x32x32_i8): PICARD_SCREEN_V3=0 keeps k_screen_oz2
+  // k_screen_oz3 (v_mfma_i32_32x32x32_i8): PICARD_SCREEN_V3=0 keeps k_screen_oz2
   bool screen_v3_ = !(std::getenv("PICARD_SCREEN_V3") && std::atoi(std::getenv("PICARD_SCREEN_V3")) == 0);
+  template <int NB>
   bool launch_screen_oz3(double alpha, double* st_rows) {
-    constexpr int NCP = 128;
-    const int U = screen3_blocks_per_step();
+    constexpr int NCP = 16 * NB;
+    const int U = screen3_blocks_per_step(NB);
     const uint64_t n_blocks = (n_local_ + 15) / 16;
     const uint64_t want = std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>((n_blocks + U - 1) / U, 1));
     const uint64_t steps_per_wg = ((n_blocks + U - 1) / U + want - 1) / want;
     const uint64_t bpw = steps_per_wg * U;
     const int nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
-    if ((bpw + 2 * (uint64_t)U) * screen2_tile_bytes(8) >= (1ull << 31) || n_blocks >= (1ull << 32)) return false;
+    if ((bpw + 2 * (uint64_t)U) * screen2_tile_bytes(NB) >= (1ull << 31) || n_blocks >= (1ull << 32)) return false;
     if (ldx % 32 != 0 || !ensure_xsf(3)) return false;
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
     if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
-    if (oz_kso() != 2) throw computation_error("int8 digit image of another layout");
+    if (oz_kso() != (NB == 8 ? 2 : 1)) throw computation_error("int8 digit image of another layout");
     Screen2Args a;
     a.xsl = d_xsl; a.xsf = d_xsf; a.wsl = d_wsl; a.wsc = d_wsc;
     a.c32 = (float)(-2.0 * alpha * fm::LOG2E);
@@ -4008,7 +4009,7 @@ struct DeviceCtx : Evaluator {
     a.ln2_alpha = fm::LN2 / alpha;
     a.bpw = (uint32_t)bpw; a.n_blocks = (uint32_t)n_blocks; a.nwg = nwg; a.partials = part;
     HIP_OK(hipEventRecord(ev[1], stream));
-    HIP_OK(screen3_launch(a, stream));
+    HIP_OK(screen3_launch(NB, a, stream));
     HIP_OK(hipEventRecord(ev[2], stream));
     k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
         part, nwg, 2 * NCP, 0, NCP, (int)kept_nc_pending, 2, st_rows, DENS_TANH, alpha, (double)n_local_, 1);
@@ -4019,8 +4020,7 @@ struct DeviceCtx : Evaluator {
   }
   template <int NB>
   void screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
-    if constexpr (NB == 8)
-      if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && screen_v3_ && launch_screen_oz3(d.alpha, st_rows)) return;
+    if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && screen_v3_ && launch_screen_oz3<NB>(d.alpha, st_rows)) return;
     if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && launch_screen_oz2<NB>(d.alpha, st_rows)) return;
     if (f32l && dmax == 3 && screen_nows_) launch_screen_oz<3, NB>(d.alpha, st_rows);
     else if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);

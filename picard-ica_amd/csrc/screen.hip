@@ -26,6 +26,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "screen2.hpp"
 
@@ -291,10 +292,19 @@ __device__ __forceinline__ v16i mfma32_i8(v4i a, v4i b, v16i c) {
   return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
 }
 
+template <int NB>
 struct S3 {
-  static constexpr int KSO = 2, U = 4, NCP = 128, TILE = SLICES * KSO * 1024;
-  static constexpr int SLOT = 4 * KSO * 1024, NBUF = 3, SCB = 256;
-  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + 2 * NCP * 2 * 8;
+  static constexpr int KSO = NB == 8 ? 2 : 1;    // k-steps of 64 features
+  static constexpr int RT = NB / 2;              // 32-row tiles
+  static constexpr int PP = 8 / RT;              // block pairs per step (one per wave and row tile)
+  static constexpr int U = 2 * PP;               // 16-sample blocks per step (NB = 8: 4, NB = 4: 8)
+  static constexpr int NCP = 16 * NB, TILE = SLICES * KSO * 1024;
+  static constexpr int PIECES = 4 * KSO;         // 1-KiB pieces per block (planes 0–3)
+  static constexpr int SLOT = PIECES * 1024, NBUF = 3, SCB = U * 64;
+  static constexpr int NSCALE = U * 64 / 256;    // scale DMAs per step (waves 8 − NSCALE … 7)
+  static constexpr int NM1 = 3 * KSO * 2, NM = 10 * KSO * 2;  // MFMAs of phase 1 (D ≤ 1) / of a step
+  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + PP * NCP * 2 * 8;
+  static_assert(U * PIECES == 32, "four pieces per wave and step");
 };
 
 // 16 row terms of a lane: q01 = P0·256 + P1, r23 = P2·256 + P3 (int32, exact) of samples r,
@@ -315,11 +325,11 @@ __device__ __forceinline__ void row_terms16(const v16i& q01, const v16i& r23, co
   }
 }
 
-// The row terms of the previous step cut into 40 slots, one after each MFMA of the current step
-// (k_screen_oz3): slots 0–15 combine element r = slot (y' = fl(fl(R23)·2^-16 + fl(Q01)), u = y'·sf),
-// 16–31 its ℓ factor ((1 + 2^−|u|·cz)/2), 32–39 the two halves of each 4-element group's end
-// (the product and its log; Σ|u| and both fp64 accumulations) — row_terms' arithmetic, element
-// for element.
+// The row terms of the previous step cut into 40 slots spread over the MFMAs of the current
+// step (k_screen_oz3): slots 0–15 combine element r = slot (y' = fl(fl(R23)·2^-16 + fl(Q01)),
+// u = y'·sf), 16–31 its ℓ factor ((1 + 2^−|u|·cz)/2), 32–39 the two halves of each 4-element
+// group's end (the product and its log; Σ|u| and both fp64 accumulations) — row_terms16's
+// arithmetic, element for element.
 struct RT3 {
   float u[16], f[16];
   float lg[4];
@@ -342,37 +352,74 @@ __device__ __forceinline__ void rt_slot(RT3& t, const v16i& q01, const v16i& r23
     g += (double)t.lg[q];
   }
 }
+// vector instructions of slot J as lowered (4 = 2 cvt + fma + mul; 3 = mul + exp + fma;
+// 4 = 3 mul + log; 7 = 3 add + 2 cvt + 2 add_f64)
+template <int J>
+constexpr int rt_slot_valu() {
+  return J < 16 ? 4 : J < 32 ? 3 : (J & 1) == 0 ? 4 : 7;
+}
 
-// schedule groups of k_screen_oz3: MFMA i, then the vector instructions of its slot
-template <int I>
+// The MFMAs of one step in order (J < NM1: D ≤ 1, products (b, a) = (0,0)→P0, (0,1)→P1,
+// (1,0)→P1 per (k-step s, chunk c); then D = 2, 3: (0,2)→P2, (0,3)→P3, (1,1)→P2, (1,2)→P3,
+// (2,0)→P2, (2,1)→P3, (3,0)→P3), each followed by its row-term slots (NB = 8: one, NB = 4: two)
+// and its schedule group.
+template <int NB>
+struct Oz3Step {
+  using S = S3<NB>;
+  static constexpr int SPM = 40 / S::NM;  // row-term slots per MFMA
+  template <int J>
+  struct Op {
+    static constexpr bool P1 = J < S::NM1;
+    static constexpr int G = P1 ? J / 3 : (J - S::NM1) / 7, I = P1 ? J % 3 : (J - S::NM1) % 7;
+    static constexpr int SS = G / 2, C = G % 2;
+    static constexpr int B = P1 ? (I == 2 ? 1 : 0) : (I < 2 ? 0 : I < 4 ? 1 : I < 6 ? 2 : 3);   // X digit
+    static constexpr int A = P1 ? (I == 1 ? 1 : 0) : (I == 0 ? 2 : I == 1 ? 3 : I == 2 ? 1 : I == 3 ? 2 : I == 4 ? 0 : I == 5 ? 1 : 0);  // W digit
+    static constexpr int D = A + B;
+    static constexpr bool FIRST = (P1 ? (I <= 1) : (I <= 1)) && G == 0;  // first MFMA into its accumulator
+  };
+};
+
+// compile-time loop: f(integral_constant<int, 0>) … f(integral_constant<int, N − 1>)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void oz3_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    oz3_for<N, I + 1>(f);
+  }
+}
+// schedule groups of k_screen_oz3: MFMA J, then the vector instructions of its slot(s) (+1 for
+// one q01 merge over the first 16 MFMAs of phase 2)
+template <int NB, int J>
 struct Oz3Groups {
-  static constexpr int NV = (I < 16 ? 4 : I < 32 ? 3 : (I & 1) == 0 ? 4 : 7) + (I >= 12 && I < 28 ? 1 : 0);
+  using S = S3<NB>;
+  static constexpr int SPM = 40 / S::NM;
+  static constexpr int NV = rt_slot_valu<J * SPM>() + (SPM == 2 ? rt_slot_valu<J * SPM + 1>() : 0) +
+                            (J >= S::NM1 && J < S::NM1 + 16 ? (SPM == 2 ? 2 : 1) : 0);
   static __device__ __forceinline__ void emit() {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-    Oz3Groups<I + 1>::emit();
+    if constexpr (J < S::NM) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+      Oz3Groups<NB, J + 1>::emit();
+    }
   }
 };
-template <>
-struct Oz3Groups<40> {
-  static __device__ __forceinline__ void emit() {}
-};
 
-template <int FILL>
+template <int NB, int FILL>
 __global__ void __launch_bounds__(512, 1)
 k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
              const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
              double* __restrict__ partials) {
-  using S = S3;
-  constexpr int U = S::U, TILE = S::TILE, SLOT = S::SLOT, NCP = S::NCP;
+  using S = S3<NB>;
+  using St = Oz3Step<NB>;
+  constexpr int KSO = S::KSO, U = S::U, TILE = S::TILE, SLOT = S::SLOT, NCP = S::NCP, RT = S::RT, PP = S::PP;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int rt = wv & 3, pp = wv >> 2;
+  const int rt = wv % RT, pp = wv / RT;
   const int n = lane & 31, gl = lane >> 5;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* tiles = smem;                         // [NBUF][U][SLOT]
-  uint8_t* scl = tiles + S::NBUF * U * SLOT;     // [NBUF][SCB]: 2 pairs × [2][16] fp32 scales
-  double* red = (double*)(scl + S::NBUF * S::SCB);  // [2][NCP][2]
+  uint8_t* tiles = smem;                             // [NBUF][U][SLOT]
+  uint8_t* scl = tiles + S::NBUF * U * SLOT;         // [NBUF][SCB]: per pair [2][16] fp32 scales
+  double* red = (double*)(scl + S::NBUF * S::SCB);   // [PP][NCP][2]
   const uint32_t b_begin = blockIdx.x * bpw;
   const uint32_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint32_t nb = b_begin < b_end ? b_end - b_begin : 0u;
@@ -381,31 +428,33 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
       uniform_ptr(xsl + (size_t)b_begin * TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * TILE)), RSRC_DW3);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
-  // DMA: wave w moves pieces 4(w & 1) … 4(w & 1) + 3 (1 KiB each) of block w >> 1 of the step;
-  // wave 7 also the step's 64 scales (one dword per lane)
-  const int bq = wv >> 1, p0 = 4 * (wv & 1);
+  // DMA: wave w moves pieces 4w … 4w + 3 of the step's 32 (block (4w) / PIECES, from piece
+  // (4w) mod PIECES: four contiguous KiB of one block); waves 8 − NSCALE … 7 also one 256-B
+  // slice of the step's scales each (one dword per lane)
+  const int bq = (4 * wv) / S::PIECES, p0 = (4 * wv) % S::PIECES;
   const uint32_t voff_x = (uint32_t)(bq * TILE + p0 * 1024 + lane * 16);
-  const bool scale_wave = wv == 7;
+  const int sw = wv - (8 - S::NSCALE);  // ≥ 0: this wave's scale slice
+  const bool scale_wave = sw >= 0;
   auto stage = [&](uint32_t step, int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bq) * SLOT + (p0 + i) * 1024), 16,
                                                (int)(voff_x + i * 1024 + step * (uint32_t)(U * TILE)), 0, 0, 0);
     if (scale_wave)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB), 4,
-                                               (int)(lane * 4 + step * (uint32_t)(U * 64)), 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB + sw * 256), 4,
+                                               (int)(sw * 256 + lane * 4 + step * (uint32_t)(U * 64)), 0, 0, 0);
   };
   // B operands: W rows 32rt + n, digits a ≤ 3, k-step s, chunk c: the 16 bytes of W-image lane
   // (n mod 16) + 16(2c + gl) of row block 2rt + n/16 (the A operand's feature map)
-  v4i wb[4][2][2];
+  v4i wb[4][KSO][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s2 = 0; s2 < KSO; ++s2)
 #pragma unroll
       for (int c = 0; c < 2; ++c)
-        wb[a][s][c] = *(const v4i*)(wsl_g + (size_t)((((2 * rt + (n >> 4)) * SLICES + a) * 2 + s) * 64 + (n & 15) +
-                                                     16 * (2 * c + gl)) * 16);
+        wb[a][s2][c] = *(const v4i*)(wsl_g + (size_t)((((2 * rt + (n >> 4)) * SLICES + a) * 2 + s2) * 64 + (n & 15) +
+                                                      16 * (2 * c + gl)) * 16);
   const double rowscale = __builtin_ldexp(wsc[rt * 32 + n], e0 - 8);  // 2^(f_i + E0 − 20)
   const float cz = __builtin_fabsf(c32) * (float)rowscale;
   // A operand of plane b, k-step s, chunk c in a staged pair: block (n >> 4) of the pair,
@@ -418,69 +467,45 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   float sfp[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) sfp[r] = 0.f;
+  auto wait_step = [&]() {  // this wave's DMA of the NEXT step landed (counted), then every wave meets
+    if (scale_wave) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
   stage(0, 0);
   stage(1, 1);
-  if (scale_wave) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  wait_step();
   uint32_t k = 0;
   int buf = 0;
   for (; k < nsteps; ++k) {
     stage(k + 2, buf == 0 ? 2 : buf - 1);  // (k + 2) mod 3; past the end: zeros, never read
     const uint8_t* pb = tiles + (buf * U + 2 * pp) * SLOT + a_lane;
-    auto ra = [&](int b, int s, int c) { return *(const v4i*)(pb + ((b * 2 + s) * 64 + 32 * c) * 16); };
+    auto ra = [&](int b, int s2, int c) { return *(const v4i*)(pb + ((b * KSO + s2) * 64 + 32 * c) * 16); };
     v16i acc[4];
     RT3 t;
-    int j = 0;  // MFMA index of the step: its row-term slot follows it
-    auto after = [&](auto jc) {
-      constexpr int J = decltype(jc)::value;
-      if constexpr (FILL > 0) rt_slot<J>(t, q01p, r23p, sfp, cz, l, g);
-    };
-    (void)j;
-    // phase 1: D ≤ 1 (12 MFMAs: slots 0–11)
-#define OZ3_P1(S_, C_, J0)                                                                       \
-    {                                                                                            \
-      const v4i x0 = ra(0, S_, C_), x1 = ra(1, S_, C_);                                          \
-      acc[0] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[0][S_][C_], v16i{}) : mfma32_i8(x0, wb[0][S_][C_], acc[0]); \
-      after(std::integral_constant<int, J0>{});                                                  \
-      acc[1] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[1][S_][C_], v16i{}) : mfma32_i8(x0, wb[1][S_][C_], acc[1]); \
-      after(std::integral_constant<int, J0 + 1>{});                                              \
-      acc[1] = mfma32_i8(x1, wb[0][S_][C_], acc[1]);                                             \
-      after(std::integral_constant<int, J0 + 2>{});                                              \
-    }
-    OZ3_P1(0, 0, 0) OZ3_P1(0, 1, 3) OZ3_P1(1, 0, 6) OZ3_P1(1, 1, 9)
-#undef OZ3_P1
+    v4i x[4];
     v16i q01;
+    auto op = [&](auto jc) {
+      constexpr int J = decltype(jc)::value;
+      using O = typename St::template Op<J>;
+      if constexpr (O::I == 0) {  // a new (k-step, chunk) group: its A operands
 #pragma unroll
-    for (int r = 0; r < 16; ++r) q01[r] = acc[0][r] * 256 + acc[1][r];
-    // phase 2: D = 2, 3 (28 MFMAs: slots 12–39)
-#define OZ3_P2(S_, C_, J0)                                                                       \
-    {                                                                                            \
-      const v4i x0 = ra(0, S_, C_), x1 = ra(1, S_, C_), x2 = ra(2, S_, C_), x3 = ra(3, S_, C_);  \
-      acc[2] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[2][S_][C_], v16i{}) : mfma32_i8(x0, wb[2][S_][C_], acc[2]); \
-      after(std::integral_constant<int, J0>{});                                                  \
-      acc[3] = (S_ == 0 && C_ == 0) ? mfma32_i8(x0, wb[3][S_][C_], v16i{}) : mfma32_i8(x0, wb[3][S_][C_], acc[3]); \
-      after(std::integral_constant<int, J0 + 1>{});                                              \
-      acc[2] = mfma32_i8(x1, wb[1][S_][C_], acc[2]);                                             \
-      after(std::integral_constant<int, J0 + 2>{});                                              \
-      acc[3] = mfma32_i8(x1, wb[2][S_][C_], acc[3]);                                             \
-      after(std::integral_constant<int, J0 + 3>{});                                              \
-      acc[2] = mfma32_i8(x2, wb[0][S_][C_], acc[2]);                                             \
-      after(std::integral_constant<int, J0 + 4>{});                                              \
-      acc[3] = mfma32_i8(x2, wb[1][S_][C_], acc[3]);                                             \
-      after(std::integral_constant<int, J0 + 5>{});                                              \
-      acc[3] = mfma32_i8(x3, wb[0][S_][C_], acc[3]);                                             \
-      after(std::integral_constant<int, J0 + 6>{});                                              \
-    }
-    OZ3_P2(0, 0, 12) OZ3_P2(0, 1, 19) OZ3_P2(1, 0, 26) OZ3_P2(1, 1, 33)
-#undef OZ3_P2
+        for (int b = 0; b < (O::P1 ? 2 : 4); ++b) x[b] = ra(b, O::SS, O::C);
+      }
+      if constexpr (O::FIRST) acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], v16i{});
+      else acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], acc[O::D]);
+      if constexpr (J == S::NM1 - 1) {  // D ≤ 1 complete: merge (spread by the schedule groups)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) q01[r] = acc[0][r] * 256 + acc[1][r];
+      }
+      if constexpr (FILL > 0) {
+        rt_slot<J * St::SPM>(t, q01p, r23p, sfp, cz, l, g);
+        if constexpr (St::SPM == 2) rt_slot<J * St::SPM + 1>(t, q01p, r23p, sfp, cz, l, g);
+      }
+    };
+    oz3_for<S::NM>(op);
     if constexpr (FILL == 0) row_terms16(q01p, r23p, sfp, cz, l, g);
-    if constexpr (FILL > 0) {
-      // the schedule: each MFMA, then its slot's vector instructions (slot sizes as lowered:
-      // 4 = 2 cvt + fma + mul; 3 = mul + exp + fma; 4 = 3 mul + log; 7 = 3 add + 2 cvt + 2 add_f64),
-      // the 16 q01 merges spread over slots 12–27
-      Oz3Groups<0>::emit();
-    }
+    if constexpr (FILL > 0) Oz3Groups<NB, 0>::emit();
     asm volatile("" ::"v"(l), "v"(g));  // the row terms stay in this block (not sunk past the wait)
 #pragma unroll
     for (int r = 0; r < 16; ++r) r23p[r] = acc[2][r] * 256 + acc[3][r];
@@ -495,9 +520,7 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
         for (int i = 0; i < 4; ++i) sfp[4 * v + i] = tv[i];
       }
     }
-    if (scale_wave) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    wait_step();
     buf = buf == 2 ? 0 : buf + 1;
   }
   row_terms16(q01p, r23p, sfp, cz, l, g);
@@ -514,7 +537,10 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
   for (int e = threadIdx.x; e < 2 * NCP; e += 512) {
     const int c = e / NCP, row = e % NCP;
-    out[e] = red[row * 2 + c] + red[(NCP + row) * 2 + c];
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < PP; ++q) v += red[(q * NCP + row) * 2 + c];
+    out[e] = v;
   }
 }
 
@@ -531,28 +557,32 @@ __global__ void __launch_bounds__(256) k_build_xsf3(const double* __restrict__ x
   }
 }
 
-template <int FILL>
+template <int NB, int FILL>
 hipError_t launch3_fill(const Screen2Args& a, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz3<FILL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             S3::LDS);
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz3<NB, FILL>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, S3<NB>::LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_screen_oz3<FILL><<<a.nwg, 512, S3::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
-                                                       a.n_blocks, a.partials);
+  k_screen_oz3<NB, FILL><<<a.nwg, 512, S3<NB>::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
+                                                                a.bpw, a.n_blocks, a.partials);
   return hipGetLastError();
 }
+// PICARD_SCREEN2_FILL=0: the row terms in the compiler's order; otherwise spread over the MFMAs
+template <int NB>
 hipError_t launch3(const Screen2Args& a, hipStream_t stream) {
-  // PICARD_SCREEN2_FILL=0: the row terms in the compiler's order; otherwise one slot per MFMA
-  return fill_knob() == 0 ? launch3_fill<0>(a, stream) : launch3_fill<1>(a, stream);
+  return fill_knob() == 0 ? launch3_fill<NB, 0>(a, stream) : launch3_fill<NB, 1>(a, stream);
 }
 }  // namespace
 
 int screen2_blocks_per_step(int nb) { return 8 / nb; }
-int screen3_blocks_per_step() { return S3::U; }
-hipError_t screen3_launch(const Screen2Args& a, hipStream_t stream) { return launch3(a, stream); }
+int screen3_blocks_per_step(int nb) { return nb == 8 ? S3<8>::U : S3<4>::U; }
+uint64_t screen3_lds_bytes(int nb) { return nb == 8 ? S3<8>::LDS : S3<4>::LDS; }
+hipError_t screen3_launch(int nb, const Screen2Args& a, hipStream_t stream) {
+  return nb == 8 ? launch3<8>(a, stream) : launch3<4>(a, stream);
+}
 hipError_t screen3_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream) {
   const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
   k_build_xsf3<<<grid ? grid : 1, 256, 0, stream>>>(xsc, n, e0, xsf);

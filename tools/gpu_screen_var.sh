@@ -1,4 +1,4 @@
-# usage: bash tools/gpu_screen_var.sh TAG — the screen kernels at (128, 2e7): k_screen_oz3
+# usage: bash tools/gpu_screen_var.sh TAG — the screen kernels at (128, 2e7) and (64, 1e7): k_screen_oz3
 # (PICARD_SCREEN2_FILL 0 / 1), k_screen_oz2 (PICARD_SCREEN_V3=0) and k_screen_oz (PICARD_SCREEN_V2=0),
 # then the screen / int8 tests on the default
 TAG=$1
@@ -8,7 +8,8 @@ mkdir -p $O
 run() {  # name, env...
   local nm=$1; shift
   env "$@" timeout -k 10 120 python3 tools/bench_loss.py 128 2e7 5 auto > $O/$nm.txt 2>&1 || { cat $O/$nm.txt; return 1; }
-  echo "$nm $(grep screen $O/$nm.txt)"
+  env "$@" timeout -k 10 120 python3 tools/bench_loss.py 64 1e7 5 auto >> $O/$nm.txt 2>&1 || { cat $O/$nm.txt; return 1; }
+  echo "$nm: $(grep screen $O/$nm.txt | sed 's/auto  //' | tr '\n' ' ')"
 }
 run oz3_fill1 PICARD_SCREEN2_FILL=1 && run oz3_fill0 PICARD_SCREEN2_FILL=0 && run oz2 PICARD_SCREEN_V3=0 && \
   run oz PICARD_SCREEN_V2=0 || exit 1
