@@ -3240,11 +3240,12 @@ struct DeviceCtx : Evaluator {
   //          + 1e-10·Σℓ. A rank whose scales leave the fp32 range (or that has no digit image)
   // runs the exact kernel into the same layout with zero bound terms: every rank issues the
   // same all-reduce, and each rank's share of the bound covers its own arithmetic.
-  // Off by default (PICARD_MULTI_F32=1 turns it on): on C4 the pass takes 31.7 ms instead of
-  // 41.2, but near convergence the tries differ by less than the fp32 bound (≈ 1e-4 in loss
-  // units), so 28 of 128 searches paid a full pass for a try the exact pass then rejected
-  // (whole fit 15.6 s against 15.0; profiles/r03_d/c4_multi_bound.txt).
-  bool multi_f32_ = std::getenv("PICARD_MULTI_F32") != nullptr;
+  // On C4 the pass takes 31.7 ms instead of 41.2, but near convergence the tries differ by less
+  // than the fp32 bound (≈ 1e-4 in loss units): used always, 28 of 128 searches paid a full pass
+  // for a try the exact pass then rejected (whole fit 15.6 s against 15.0; profiles/r03_d/
+  // c4_multi_bound.txt). The solver therefore uses it only until the first such search
+  // (Solver::multi_bound_on_); PICARD_MULTI_F32=0 turns it off here.
+  bool multi_f32_ = !(std::getenv("PICARD_MULTI_F32") && std::atoi(std::getenv("PICARD_MULTI_F32")) == 0);
   bool eval_loss_multi_bound(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
                              const double* alphas, int na, double* ll_out, double* bnd_out) override {
     if (!multi_f32_ || !multi_loss_ok(nc, d) || d.kind != DENS_TANH || want_y2 || na > ML_NA || yw_ks(nf) == 0)

@@ -545,7 +545,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       // without Σy² in the loss (not extended), the tries may come with a bound instead of
       // exact sums (fp32 row terms); every decision is then taken on exact values (below)
       bool bounded = false;
-      if (!extended_) {
+      if (!extended_ && multi_bound_on_) {
         bnd.assign(na * n, 0.0);
         bounded = ev_->eval_loss_multi_bound(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
                                              alphas.data(), (int)na, ll.data(), bnd.data());
@@ -601,6 +601,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
                 r.step = scale(direction, a);
                 return r;
               }
+              multi_bound_on_ = false;  // a full pass spent on a rejected try: exact tries from now on
               if (j + 1 == na) {  // kept below: step() needs no second pass at the same W
                 last_full = std::move(full);
                 have_last_full = true;

@@ -142,6 +142,10 @@ class Solver {
   // Non-ortho searches evaluate tries >= 2 in one multi-α pass
   // (Evaluator::eval_loss_multi) unless PICARD_NO_MULTI=1.
   bool no_multi_ = false;
+  // the bounded (fp32) multi-try pass is used until a search pays a full pass for a try the exact
+  // pass then rejects (near convergence the tries differ by less than its bound): from then on
+  // the exact multi-try pass. Decided from reduced statistics only: the same on every rank.
+  bool multi_bound_on_ = true;
   // PICARD_TRACE timing: evaluator calls, try-1 map, waits for the helper's maps
   double eval_ms_ = 0.0, map1_ms_ = 0.0, ahead_wait_ms_ = 0.0;
   bool trace_ = false;  // PICARD_TRACE=1: one stderr line per iteration (line-search tries)
