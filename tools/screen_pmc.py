@@ -8,6 +8,18 @@ import sys
 from collections import defaultdict
 
 
+def kname(raw):
+    """Kernel name without return type, namespaces or parameter list (template arguments kept)."""
+    k = raw.replace("(anonymous namespace)::", "").replace("pcamd::", "").replace("void ", "")
+    depth = 0
+    for i, ch in enumerate(k):
+        depth += ch == "<"
+        depth -= ch == ">"
+        if ch == "(" and depth == 0:
+            return k[:i].strip()
+    return k.strip()
+
+
 def main():
     d = sys.argv[1]
     cnt = defaultdict(lambda: defaultdict(list))
@@ -15,11 +27,11 @@ def main():
     for p in ("p1", "p2", "p3"):
         for f in glob.glob(os.path.join(d, p, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pcamd::", "")
+                k = kname(r["Kernel_Name"])
                 cnt[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for f in glob.glob(os.path.join(d, p, "**", "*kernel_trace.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pcamd::", "")
+                k = kname(r["Kernel_Name"])
                 dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     for k, v in cnt.items():
         c = {n: sum(x) / len(x) for n, x in v.items()}
