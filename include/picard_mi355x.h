@@ -248,10 +248,10 @@ int pc_ctx_eval_loss_multi(pc_ctx* ctx, const double* w, const double* z, uint64
 /* The same tries with their row terms in fp32 and a rigorous bound instead of exact sums
  * (tanh, the int8 stage at n_features ≤ 256; the non-orthogonal line search of a
  * non-extended fit, whose loss needs no Σy²): |Σℓ_j,i − ll_out[j·nc + i]| ≤ bnd_out[j·nc + i]
- * where Σℓ_j,i is what pc_ctx_eval_loss gives at w + α_j·z. n_alpha ≤ 12. PICARD_MULTI_F32=0
- * disables it (the solver uses it until a search pays a full pass for a try the exact pass then
- * rejects). Returns PC_ERR_UNSUPPORTED where it does not apply (the caller then uses
- * pc_ctx_eval_loss_multi). */
+ * where Σℓ_j,i is what pc_ctx_eval_loss gives at w + α_j·z. n_alpha ≤ 12. Opt-in:
+ * PICARD_MULTI_F32=1 (the solver then uses it until a search pays a full pass for a try the exact
+ * pass rejects). Returns PC_ERR_UNSUPPORTED where it does not apply or is not
+ * enabled (the caller then uses pc_ctx_eval_loss_multi). */
 int pc_ctx_eval_loss_multi_bound(pc_ctx* ctx, const double* w, const double* z, uint64_t nc, const double* mu,
                                  pc_density density, const double* alphas, uint64_t n_alpha, double* ll_out,
                                  double* bnd_out, char* err, size_t errlen);

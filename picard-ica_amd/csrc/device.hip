@@ -3243,9 +3243,10 @@ struct DeviceCtx : Evaluator {
   // On C4 the pass takes 31.7 ms instead of 41.2, but near convergence the tries differ by less
   // than the fp32 bound (≈ 1e-4 in loss units): used always, 28 of 128 searches paid a full pass
   // for a try the exact pass then rejected (whole fit 15.6 s against 15.0; profiles/r03_d/
-  // c4_multi_bound.txt). The solver therefore uses it only until the first such search
-  // (Solver::multi_bound_on_); PICARD_MULTI_F32=0 turns it off here.
-  bool multi_f32_ = !(std::getenv("PICARD_MULTI_F32") && std::atoi(std::getenv("PICARD_MULTI_F32")) == 0);
+  // c4_multi_bound.txt). Used only until the first such search (Solver::multi_bound_on_), the
+  // fit took 15.30 s against 15.12 s exact (profiles/r04_b/c4_policy.txt): no gain either, so it
+  // stays opt-in (PICARD_MULTI_F32=1).
+  bool multi_f32_ = std::getenv("PICARD_MULTI_F32") && std::atoi(std::getenv("PICARD_MULTI_F32")) == 1;
   bool eval_loss_multi_bound(const double* w, const double* z, size_t nc, const double* mu, pc_density d,
                              const double* alphas, int na, double* ll_out, double* bnd_out) override {
     if (!multi_f32_ || !multi_loss_ok(nc, d) || d.kind != DENS_TANH || want_y2 || na > ML_NA || yw_ks(nf) == 0)
@@ -3987,8 +3988,9 @@ struct DeviceCtx : Evaluator {
     ++n_screen_passes_;
     return true;
   }
-  // k_screen_oz3 (v_mfma_i32_32x32x32_i8): PICARD_SCREEN_V3=0 keeps k_screen_oz2
-  bool screen_v3_ = !(std::getenv("PICARD_SCREEN_V3") && std::atoi(std::getenv("PICARD_SCREEN_V3")) == 0);
+  // k_screen_oz3 (v_mfma_i32_32x32x32_i8): opt-in (PICARD_SCREEN_V3=1); measured no faster than
+  // k_screen_oz2 (profiles/r04_b), and its NB = 4 form fails the bound test at n = 40
+  bool screen_v3_ = std::getenv("PICARD_SCREEN_V3") && std::atoi(std::getenv("PICARD_SCREEN_V3")) == 1;
   template <int NB>
   bool launch_screen_oz3(double alpha, double* st_rows) {
     constexpr int NCP = 16 * NB;

@@ -267,11 +267,14 @@ hipError_t launch(const Screen2Args& a, hipStream_t stream) {
 
 
 // ---------------------------------------------------------------------------------------------
-// k_screen_oz3 (NB = 8: 64 < nc ≤ 128, nf ≤ 128): the same screen on v_mfma_i32_32x32x32_i8.
-// That MFMA runs 32 cycles for the MACs of two 16x16x64 but holds its wave's vector issue for
-// only ≈ 8–10 of them (tools/microbench/fill_coexec.hip, profiles/r04_a: 4 fp32 FMAs ride along
-// in 34 cycles), so the row terms of the previous step fit in the gaps of the current step's
-// MFMAs and the kernel runs at the matrix pipe instead of at the issue port.
+// k_screen_oz3 (NB = 8: 64 < nc ≤ 128, nf ≤ 128; NB = 4: 32 < nc ≤ 64, nf ≤ 64): the same screen
+// on v_mfma_i32_32x32x32_i8. That MFMA runs 32 cycles for the MACs of two 16x16x64 but holds its
+// wave's vector issue for only ≈ 8–10 of them (tools/microbench/fill_coexec.hip, profiles/r04_a:
+// 4 fp32 FMAs ride along in 34 cycles), so the row terms of the previous unit fit in the gaps of
+// the current unit's MFMAs. ONE wave per SIMD (4 waves, one workgroup per CU): a second wave whose
+// next instruction is an MFMA waiting for the pipe blocks the first wave's vector issue
+// (tools/microbench/agpr_coexec.hip), which is what kept the 8-wave form of this kernel at the
+// speed of k_screen_oz2 (profiles/r04_b).
 //
 // Operands (no new X image): the 32x32x32 A operand of 32 samples × 32 features is read from the
 // 16x16x64 digit image of two blocks — lane l takes the 16 bytes of image lane
@@ -283,8 +286,9 @@ hipError_t launch(const Screen2Args& a, hipStream_t stream) {
 // (sample σ(m mod 16) = ((m mod 16) >> 2) + 4((m mod 16) & 3), ozaki.inc).
 // Per element the arithmetic of row_terms (so the same bound); the Σ|u| partial sums group 4
 // samples as there, each 4-sample product of (1 + 2^−z)/2 gets one log.
-// 8 waves, one workgroup per CU (≈ 230 VGPRs per wave): wave w takes row tile rt = w & 3 and pair
-// pp = w >> 2 of every step (4 blocks, 64 samples).
+// Work units: (32-row tile rt, block pair pp) of a step; a step holds 8 units (NB = 8: 4 tiles ×
+// 2 pairs, NB = 4: 2 × 4), wave w takes tile rt = w mod RT and the pairs w / RT + (4 / RT)·j,
+// j < 2, one after the other — each unit's MFMAs carry the previous unit's row terms.
 // ---------------------------------------------------------------------------------------------
 typedef int v16i __attribute__((ext_vector_type(16)));
 
@@ -296,15 +300,19 @@ template <int NB>
 struct S3 {
   static constexpr int KSO = NB == 8 ? 2 : 1;    // k-steps of 64 features
   static constexpr int RT = NB / 2;              // 32-row tiles
-  static constexpr int PP = 8 / RT;              // block pairs per step (one per wave and row tile)
+  static constexpr int PP = 8 / RT;              // block pairs per step
   static constexpr int U = 2 * PP;               // 16-sample blocks per step (NB = 8: 4, NB = 4: 8)
+  static constexpr int WAVES = 4;                // one per SIMD
+  static constexpr int WPR = WAVES / RT;         // waves per row tile (NB = 8: 1, NB = 4: 2)
+  static constexpr int UPW = RT * PP / WAVES;    // units per wave and step
   static constexpr int NCP = 16 * NB, TILE = SLICES * KSO * 1024;
   static constexpr int PIECES = 4 * KSO;         // 1-KiB pieces per block (planes 0–3)
   static constexpr int SLOT = PIECES * 1024, NBUF = 3, SCB = U * 64;
-  static constexpr int NSCALE = U * 64 / 256;    // scale DMAs per step (waves 8 − NSCALE … 7)
-  static constexpr int NM1 = 3 * KSO * 2, NM = 10 * KSO * 2;  // MFMAs of phase 1 (D ≤ 1) / of a step
-  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + PP * NCP * 2 * 8;
-  static_assert(U * PIECES == 32, "four pieces per wave and step");
+  static constexpr int PPW = U * PIECES / WAVES; // DMA pieces per wave and step
+  static constexpr int NSCALE = U * 64 / 256;    // scale DMAs per step (waves 4 − NSCALE … 3)
+  static constexpr int NM1 = 3 * KSO * 2, NM = 10 * KSO * 2;  // MFMAs of phase 1 (D ≤ 1) / of a unit
+  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + WPR * NCP * 2 * 8;
+  static_assert(U * PIECES == 32 && UPW == 2 && PPW == 8 && NSCALE >= 1, "eight pieces per wave and step");
 };
 
 // 16 row terms of a lane: q01 = P0·256 + P1, r23 = P2·256 + P3 (int32, exact) of samples r,
@@ -405,21 +413,22 @@ struct Oz3Groups {
 };
 
 template <int NB, int FILL>
-__global__ void __launch_bounds__(512, 1)
+__global__ void __launch_bounds__(256, 1)
 k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
              const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
              double* __restrict__ partials) {
   using S = S3<NB>;
   using St = Oz3Step<NB>;
-  constexpr int KSO = S::KSO, U = S::U, TILE = S::TILE, SLOT = S::SLOT, NCP = S::NCP, RT = S::RT, PP = S::PP;
+  constexpr int KSO = S::KSO, U = S::U, TILE = S::TILE, SLOT = S::SLOT, NCP = S::NCP, RT = S::RT, WPR = S::WPR;
+  constexpr int PIECES = S::PIECES;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int rt = wv % RT, pp = wv / RT;
+  const int rt = wv % RT, wq = wv / RT;
   const int n = lane & 31, gl = lane >> 5;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* tiles = smem;                             // [NBUF][U][SLOT]
   uint8_t* scl = tiles + S::NBUF * U * SLOT;         // [NBUF][SCB]: per pair [2][16] fp32 scales
-  double* red = (double*)(scl + S::NBUF * S::SCB);   // [PP][NCP][2]
+  double* red = (double*)(scl + S::NBUF * S::SCB);   // [WPR][NCP][2]
   const uint32_t b_begin = blockIdx.x * bpw;
   const uint32_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
   const uint32_t nb = b_begin < b_end ? b_end - b_begin : 0u;
@@ -428,18 +437,19 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
       uniform_ptr(xsl + (size_t)b_begin * TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * TILE)), RSRC_DW3);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
-  // DMA: wave w moves pieces 4w … 4w + 3 of the step's 32 (block (4w) / PIECES, from piece
-  // (4w) mod PIECES: four contiguous KiB of one block); waves 8 − NSCALE … 7 also one 256-B
-  // slice of the step's scales each (one dword per lane)
-  const int bq = (4 * wv) / S::PIECES, p0 = (4 * wv) % S::PIECES;
-  const uint32_t voff_x = (uint32_t)(bq * TILE + p0 * 1024 + lane * 16);
-  const int sw = wv - (8 - S::NSCALE);  // ≥ 0: this wave's scale slice
+  // DMA: wave w moves pieces 8w … 8w + 7 of the step's 32 (piece p of the step: block p / PIECES,
+  // digit-image KiB p mod PIECES; in LDS the step's pieces are contiguous); waves 4 − NSCALE … 3
+  // also one 256-B slice of the step's scales each (one dword per lane)
+  const uint32_t voff_x = (uint32_t)((S::PPW * wv / PIECES) * TILE + lane * 16);
+  const int sw = wv - (S::WAVES - S::NSCALE);  // ≥ 0: this wave's scale slice
   const bool scale_wave = sw >= 0;
   auto stage = [&](uint32_t step, int buf) {
+    uint8_t* dst = tiles + buf * U * SLOT + S::PPW * wv * 1024;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bq) * SLOT + (p0 + i) * 1024), 16,
-                                               (int)(voff_x + i * 1024 + step * (uint32_t)(U * TILE)), 0, 0, 0);
+    for (int i = 0; i < S::PPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, (lds_vptr2)(dst + i * 1024), 16,
+          (int)(voff_x + (i / PIECES) * TILE + (i % PIECES) * 1024 + step * (uint32_t)(U * TILE)), 0, 0, 0);
     if (scale_wave)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB + sw * 256), 4,
                                                (int)(sw * 256 + lane * 4 + step * (uint32_t)(U * 64)), 0, 0, 0);
@@ -461,57 +471,59 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   // image lane (n & 15) + 16(2c + gl)
   const uint32_t a_lane = (uint32_t)((n >> 4) * SLOT + ((n & 15) + 16 * gl) * 16);
   double l = 0.0, g = 0.0;
-  v16i q01p, r23p;  // the previous step's merged diagonals (zero before step 0: zero terms)
+  v16i q01p, r23p;  // the previous unit's merged diagonals (zero before the first: zero terms)
 #pragma unroll
   for (int r = 0; r < 16; ++r) q01p[r] = r23p[r] = 0;
   float sfp[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) sfp[r] = 0.f;
   auto wait_step = [&]() {  // this wave's DMA of the NEXT step landed (counted), then every wave meets
-    if (scale_wave) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    if (scale_wave) asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
   stage(0, 0);
   stage(1, 1);
   wait_step();
-  uint32_t k = 0;
   int buf = 0;
-  for (; k < nsteps; ++k) {
+  for (uint32_t k = 0; k < nsteps; ++k) {
     stage(k + 2, buf == 0 ? 2 : buf - 1);  // (k + 2) mod 3; past the end: zeros, never read
-    const uint8_t* pb = tiles + (buf * U + 2 * pp) * SLOT + a_lane;
-    auto ra = [&](int b, int s2, int c) { return *(const v4i*)(pb + ((b * KSO + s2) * 64 + 32 * c) * 16); };
-    v16i acc[4];
-    RT3 t;
-    v4i x[4];
-    v16i q01;
-    auto op = [&](auto jc) {
-      constexpr int J = decltype(jc)::value;
-      using O = typename St::template Op<J>;
-      if constexpr (O::I == 0) {  // a new (k-step, chunk) group: its A operands
 #pragma unroll
-        for (int b = 0; b < (O::P1 ? 2 : 4); ++b) x[b] = ra(b, O::SS, O::C);
-      }
-      if constexpr (O::FIRST) acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], v16i{});
-      else acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], acc[O::D]);
-      if constexpr (J == S::NM1 - 1) {  // D ≤ 1 complete: merge (spread by the schedule groups)
+    for (int j = 0; j < S::UPW; ++j) {
+      const int pp = wq + WPR * j;
+      const uint8_t* pb = tiles + (buf * U + 2 * pp) * SLOT + a_lane;
+      auto ra = [&](int b, int s2, int c) { return *(const v4i*)(pb + ((b * KSO + s2) * 64 + 32 * c) * 16); };
+      v16i acc[4];
+      RT3 t;
+      v4i x[4];
+      v16i q01;
+      auto op = [&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        using O = typename St::template Op<J>;
+        if constexpr (O::I == 0) {  // a new (k-step, chunk) group: its A operands
 #pragma unroll
-        for (int r = 0; r < 16; ++r) q01[r] = acc[0][r] * 256 + acc[1][r];
-      }
-      if constexpr (FILL > 0) {
-        rt_slot<J * St::SPM>(t, q01p, r23p, sfp, cz, l, g);
-        if constexpr (St::SPM == 2) rt_slot<J * St::SPM + 1>(t, q01p, r23p, sfp, cz, l, g);
-      }
-    };
-    oz3_for<S::NM>(op);
-    if constexpr (FILL == 0) row_terms16(q01p, r23p, sfp, cz, l, g);
-    if constexpr (FILL > 0) Oz3Groups<NB, 0>::emit();
-    asm volatile("" ::"v"(l), "v"(g));  // the row terms stay in this block (not sunk past the wait)
+          for (int b = 0; b < (O::P1 ? 2 : 4); ++b) x[b] = ra(b, O::SS, O::C);
+        }
+        if constexpr (O::FIRST) acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], v16i{});
+        else acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], acc[O::D]);
+        if constexpr (J == S::NM1 - 1) {  // D ≤ 1 complete: merge (spread by the schedule groups)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) r23p[r] = acc[2][r] * 256 + acc[3][r];
-    q01p = q01;
-    // this step's scales: pair pp, lane group gl — 16 floats (the layout of k_build_xsf3)
-    {
+          for (int r = 0; r < 16; ++r) q01[r] = acc[0][r] * 256 + acc[1][r];
+        }
+        if constexpr (FILL > 0) {
+          rt_slot<J * St::SPM>(t, q01p, r23p, sfp, cz, l, g);
+          if constexpr (St::SPM == 2) rt_slot<J * St::SPM + 1>(t, q01p, r23p, sfp, cz, l, g);
+        }
+      };
+      oz3_for<S::NM>(op);
+      if constexpr (FILL == 0) row_terms16(q01p, r23p, sfp, cz, l, g);
+      if constexpr (FILL > 0) Oz3Groups<NB, 0>::emit();
+      asm volatile("" ::"v"(l), "v"(g));  // the row terms stay in this unit (not sunk past the wait)
+      __builtin_amdgcn_sched_barrier(0);  // each unit its own scheduling region
+#pragma unroll
+      for (int r = 0; r < 16; ++r) r23p[r] = acc[2][r] * 256 + acc[3][r];
+      q01p = q01;
+      // this unit's scales: pair pp, lane group gl — 16 floats (the layout of k_build_xsf3)
       const float* sp = (const float*)(scl + buf * S::SCB) + pp * 32 + gl * 16;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -530,16 +542,16 @@ k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   rs_ll += __shfl_xor(rs_ll, 32);
   rs_y += __shfl_xor(rs_y, 32);
   if (gl == 0) {
-    red[(pp * NCP + rt * 32 + n) * 2 + 0] = rs_ll;
-    red[(pp * NCP + rt * 32 + n) * 2 + 1] = rs_y;
+    red[(wq * NCP + rt * 32 + n) * 2 + 0] = rs_ll;
+    red[(wq * NCP + rt * 32 + n) * 2 + 1] = rs_y;
   }
   __syncthreads();
   double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
-  for (int e = threadIdx.x; e < 2 * NCP; e += 512) {
+  for (int e = threadIdx.x; e < 2 * NCP; e += 256) {
     const int c = e / NCP, row = e % NCP;
     double v = 0.0;
 #pragma unroll
-    for (int q = 0; q < PP; ++q) v += red[(q * NCP + row) * 2 + c];
+    for (int q = 0; q < WPR; ++q) v += red[(q * NCP + row) * 2 + c];
     out[e] = v;
   }
 }
@@ -566,7 +578,7 @@ hipError_t launch3_fill(const Screen2Args& a, hipStream_t stream) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_screen_oz3<NB, FILL><<<a.nwg, 512, S3<NB>::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
+  k_screen_oz3<NB, FILL><<<a.nwg, 256, S3<NB>::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
                                                                 a.bpw, a.n_blocks, a.partials);
   return hipGetLastError();
 }

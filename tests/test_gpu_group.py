@@ -220,8 +220,8 @@ def test_group_divergent_collectives_fail_fast(pa):
 
 
 def test_group_unsupported_is_not_an_abort(pa, monkeypatch):
-    """A capability miss (PC_ERR_UNSUPPORTED: the bounded multi-try pass with PICARD_MULTI_F32=0, a screen for a density without one, device JADE sweeps for a shape that does not
-    fit) leaves the group usable: the documented fallback (pc_ctx_eval_loss_multi, an exact
+    """A capability miss (PC_ERR_UNSUPPORTED: the bounded multi-try pass without PICARD_MULTI_F32=1, a screen for a density
+    without one, device JADE sweeps for a shape that does not fit) leaves the group usable: the documented fallback (pc_ctx_eval_loss_multi, an exact
     try) then runs on every rank and matches world = 1."""
     monkeypatch.setenv("PICARD_MULTI_F32", "0")
     nf, T = 96, 40009
