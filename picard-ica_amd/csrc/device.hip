@@ -3568,11 +3568,10 @@ struct DeviceCtx : Evaluator {
   float* d_xsf = nullptr;
   size_t cap_xsf_ = 0;
   int xsf_e0_ = INT_MIN;
-  int xsf_layout_ = 0;  // 2: k_build_xsf (k_screen_oz2), 3: k_build_xsf3 (k_screen_oz3)
   // false when the second screen cannot run here (the caller uses k_screen_oz)
-  bool ensure_xsf(int layout = 2) {
+  bool ensure_xsf() {
     if (!xsc_range_ok_ || xsc_emax_ - xsc_emin_ > 100) return false;  // u = y'·2^(e_t − E0) stays normal
-    if (xsf_e0_ == xsc_emax_ && d_xsf && xsf_layout_ == layout) return true;
+    if (xsf_e0_ == xsc_emax_ && d_xsf) return true;
     if (cap_xsf_ < ldx) {
       if (d_xsf) (void)t_free(d_xsf);
       d_xsf = nullptr;
@@ -3584,10 +3583,8 @@ struct DeviceCtx : Evaluator {
       }
       cap_xsf_ = ldx;
     }
-    if (layout == 3) HIP_OK(screen3_build_xsf(d_xsc, ldx, xsc_emax_, d_xsf, stream));
-    else HIP_OK(screen2_build_xsf(d_xsc, ldx, xsc_emax_, d_xsf, stream));
+    HIP_OK(screen2_build_xsf(d_xsc, ldx, xsc_emax_, d_xsf, stream));
     xsf_e0_ = xsc_emax_;
-    xsf_layout_ = layout;
     return true;
   }
   // the shapes the i8 loss kernel covers: 64 < nc ≤ 128, nf ≤ 128, centred X
@@ -3968,7 +3965,7 @@ struct DeviceCtx : Evaluator {
     const int nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
     // 32-bit buffer offsets within a workgroup's range (and the kernel's 32-bit block counts)
     if ((bpw + 2 * (uint64_t)U) * screen2_tile_bytes(NB) >= (1ull << 31) || n_blocks >= (1ull << 32)) return false;
-    if (!ensure_xsf(2)) return false;
+    if (!ensure_xsf()) return false;
     double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
     if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
     if (oz_kso() != (NB == 8 ? 2 : 1)) throw computation_error("int8 digit image of another layout");
@@ -3988,42 +3985,8 @@ struct DeviceCtx : Evaluator {
     ++n_screen_passes_;
     return true;
   }
-  // k_screen_oz3 (v_mfma_i32_32x32x32_i8): opt-in (PICARD_SCREEN_V3=1); measured no faster than
-  // k_screen_oz2 (profiles/r04_b), and its NB = 4 form fails the bound test at n = 40
-  bool screen_v3_ = std::getenv("PICARD_SCREEN_V3") && std::atoi(std::getenv("PICARD_SCREEN_V3")) == 1;
-  template <int NB>
-  bool launch_screen_oz3(double alpha, double* st_rows) {
-    constexpr int NCP = 16 * NB;
-    const int U = screen3_blocks_per_step(NB);
-    const uint64_t n_blocks = (n_local_ + 15) / 16;
-    const uint64_t want = std::min<uint64_t>((uint64_t)n_cu, std::max<uint64_t>((n_blocks + U - 1) / U, 1));
-    const uint64_t steps_per_wg = ((n_blocks + U - 1) / U + want - 1) / want;
-    const uint64_t bpw = steps_per_wg * U;
-    const int nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
-    if ((bpw + 2 * (uint64_t)U) * screen2_tile_bytes(NB) >= (1ull << 31) || n_blocks >= (1ull << 32)) return false;
-    if (ldx % 32 != 0 || !ensure_xsf(3)) return false;
-    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
-    if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
-    if (oz_kso() != (NB == 8 ? 2 : 1)) throw computation_error("int8 digit image of another layout");
-    Screen2Args a;
-    a.xsl = d_xsl; a.xsf = d_xsf; a.wsl = d_wsl; a.wsc = d_wsc;
-    a.c32 = (float)(-2.0 * alpha * fm::LOG2E);
-    a.e0 = xsf_e0_;
-    a.ln2_alpha = fm::LN2 / alpha;
-    a.bpw = (uint32_t)bpw; a.n_blocks = (uint32_t)n_blocks; a.nwg = nwg; a.partials = part;
-    HIP_OK(hipEventRecord(ev[1], stream));
-    HIP_OK(screen3_launch(NB, a, stream));
-    HIP_OK(hipEventRecord(ev[2], stream));
-    k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
-        part, nwg, 2 * NCP, 0, NCP, (int)kept_nc_pending, 2, st_rows, DENS_TANH, alpha, (double)n_local_, 1);
-    HIP_OK(hipGetLastError());
-    ++n_int8_passes_;
-    ++n_screen_passes_;
-    return true;
-  }
   template <int NB>
   void screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
-    if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && screen_v3_ && launch_screen_oz3<NB>(d.alpha, st_rows)) return;
     if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && launch_screen_oz2<NB>(d.alpha, st_rows)) return;
     if (f32l && dmax == 3 && screen_nows_) launch_screen_oz<3, NB>(d.alpha, st_rows);
     else if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);

@@ -266,340 +266,9 @@ hipError_t launch(const Screen2Args& a, hipStream_t stream) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// k_screen_oz3 (NB = 8: 64 < nc ≤ 128, nf ≤ 128; NB = 4: 32 < nc ≤ 64, nf ≤ 64): the same screen
-// on v_mfma_i32_32x32x32_i8. That MFMA runs 32 cycles for the MACs of two 16x16x64 but holds its
-// wave's vector issue for only ≈ 8–10 of them (tools/microbench/fill_coexec.hip, profiles/r04_a:
-// 4 fp32 FMAs ride along in 34 cycles), so the row terms of the previous unit fit in the gaps of
-// the current unit's MFMAs. ONE wave per SIMD (4 waves, one workgroup per CU): a second wave whose
-// next instruction is an MFMA waiting for the pipe blocks the first wave's vector issue
-// (tools/microbench/agpr_coexec.hip), which is what kept the 8-wave form of this kernel at the
-// speed of k_screen_oz2 (profiles/r04_b).
-//
-// Operands (no new X image): the 32x32x32 A operand of 32 samples × 32 features is read from the
-// 16x16x64 digit image of two blocks — lane l takes the 16 bytes of image lane
-// (l mod 16) + 16·(2c + l/32) of block (l mod 32)/16 (chunk c of the k-step) — and the B operand
-// (W) is gathered from the W digit image with the same feature ↔ (lane group, byte) map, so both
-// operands agree on every feature whatever order the instruction sums them in. Output (32 × 32
-// i32, 16 registers): lane l holds W row 32·rt + (l mod 32) and the 16 samples-rows
-// m = 8(r/4) + 4(l/32) + (r mod 4) of the pair, i.e. block m/16 of the pair, image row m mod 16
-// (sample σ(m mod 16) = ((m mod 16) >> 2) + 4((m mod 16) & 3), ozaki.inc).
-// Per element the arithmetic of row_terms (so the same bound); the Σ|u| partial sums group 4
-// samples as there, each 4-sample product of (1 + 2^−z)/2 gets one log.
-// Work units: (32-row tile rt, block pair pp) of a step; a step holds 8 units (NB = 8: 4 tiles ×
-// 2 pairs, NB = 4: 2 × 4), wave w takes tile rt = w mod RT and the pairs w / RT + (4 / RT)·j,
-// j < 2, one after the other — each unit's MFMAs carry the previous unit's row terms.
-// ---------------------------------------------------------------------------------------------
-typedef int v16i __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ v16i mfma32_i8(v4i a, v4i b, v16i c) {
-  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
-}
-
-template <int NB>
-struct S3 {
-  static constexpr int KSO = NB == 8 ? 2 : 1;    // k-steps of 64 features
-  static constexpr int RT = NB / 2;              // 32-row tiles
-  static constexpr int PP = 8 / RT;              // block pairs per step
-  static constexpr int U = 2 * PP;               // 16-sample blocks per step (NB = 8: 4, NB = 4: 8)
-  static constexpr int WAVES = 4;                // one per SIMD
-  static constexpr int WPR = WAVES / RT;         // waves per row tile (NB = 8: 1, NB = 4: 2)
-  static constexpr int UPW = RT * PP / WAVES;    // units per wave and step
-  static constexpr int NCP = 16 * NB, TILE = SLICES * KSO * 1024;
-  static constexpr int PIECES = 4 * KSO;         // 1-KiB pieces per block (planes 0–3)
-  static constexpr int SLOT = PIECES * 1024, NBUF = 3, SCB = U * 64;
-  static constexpr int PPW = U * PIECES / WAVES; // DMA pieces per wave and step
-  static constexpr int NSCALE = U * 64 / 256;    // scale DMAs per step (waves 4 − NSCALE … 3)
-  static constexpr int NM1 = 3 * KSO * 2, NM = 10 * KSO * 2;  // MFMAs of phase 1 (D ≤ 1) / of a unit
-  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + WPR * NCP * 2 * 8;
-  static_assert(U * PIECES == 32 && UPW == 2 && PPW == 8 && NSCALE >= 1, "eight pieces per wave and step");
-};
-
-// 16 row terms of a lane: q01 = P0·256 + P1, r23 = P2·256 + P3 (int32, exact) of samples r,
-// scales sf[r] = 2^(e_t − E0)
-__device__ __forceinline__ void row_terms16(const v16i& q01, const v16i& r23, const float (&sf)[16], float cz,
-                                            double& l, double& g) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float u[4], f[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * q + i;
-      u[i] = __builtin_fmaf((float)r23[r], 0x1p-16f, (float)q01[r]) * sf[r];
-      f[i] = __builtin_fmaf(__builtin_amdgcn_exp2f(-(__builtin_fabsf(u[i]) * cz)), 0.5f, 0.5f);
-    }
-    l += (double)((__builtin_fabsf(u[0]) + __builtin_fabsf(u[1])) + (__builtin_fabsf(u[2]) + __builtin_fabsf(u[3])));
-    g += (double)__builtin_amdgcn_logf((f[0] * f[1]) * (f[2] * f[3]));
-  }
-}
-
-// The row terms of the previous step cut into 40 slots spread over the MFMAs of the current
-// step (k_screen_oz3): slots 0–15 combine element r = slot (y' = fl(fl(R23)·2^-16 + fl(Q01)),
-// u = y'·sf), 16–31 its ℓ factor ((1 + 2^−|u|·cz)/2), 32–39 the two halves of each 4-element
-// group's end (the product and its log; Σ|u| and both fp64 accumulations) — row_terms16's
-// arithmetic, element for element.
-struct RT3 {
-  float u[16], f[16];
-  float lg[4];
-};
-template <int J>
-__device__ __forceinline__ void rt_slot(RT3& t, const v16i& q01, const v16i& r23, const float (&sf)[16], float cz,
-                                        double& l, double& g) {
-  if constexpr (J < 16) {
-    t.u[J] = __builtin_fmaf((float)r23[J], 0x1p-16f, (float)q01[J]) * sf[J];
-  } else if constexpr (J < 32) {
-    constexpr int r = J - 16;
-    t.f[r] = __builtin_fmaf(__builtin_amdgcn_exp2f(-(__builtin_fabsf(t.u[r]) * cz)), 0.5f, 0.5f);
-  } else if constexpr ((J & 1) == 0) {
-    constexpr int q = (J - 32) >> 1;
-    t.lg[q] = __builtin_amdgcn_logf((t.f[4 * q] * t.f[4 * q + 1]) * (t.f[4 * q + 2] * t.f[4 * q + 3]));
-  } else {
-    constexpr int q = (J - 32) >> 1;
-    l += (double)((__builtin_fabsf(t.u[4 * q]) + __builtin_fabsf(t.u[4 * q + 1])) +
-                  (__builtin_fabsf(t.u[4 * q + 2]) + __builtin_fabsf(t.u[4 * q + 3])));
-    g += (double)t.lg[q];
-  }
-}
-// vector instructions of slot J as lowered (4 = 2 cvt + fma + mul; 3 = mul + exp + fma;
-// 4 = 3 mul + log; 7 = 3 add + 2 cvt + 2 add_f64)
-template <int J>
-constexpr int rt_slot_valu() {
-  return J < 16 ? 4 : J < 32 ? 3 : (J & 1) == 0 ? 4 : 7;
-}
-
-// The MFMAs of one step in order (J < NM1: D ≤ 1, products (b, a) = (0,0)→P0, (0,1)→P1,
-// (1,0)→P1 per (k-step s, chunk c); then D = 2, 3: (0,2)→P2, (0,3)→P3, (1,1)→P2, (1,2)→P3,
-// (2,0)→P2, (2,1)→P3, (3,0)→P3), each followed by its row-term slots (NB = 8: one, NB = 4: two)
-// and its schedule group.
-template <int NB>
-struct Oz3Step {
-  using S = S3<NB>;
-  static constexpr int SPM = 40 / S::NM;  // row-term slots per MFMA
-  template <int J>
-  struct Op {
-    static constexpr bool P1 = J < S::NM1;
-    static constexpr int G = P1 ? J / 3 : (J - S::NM1) / 7, I = P1 ? J % 3 : (J - S::NM1) % 7;
-    static constexpr int SS = G / 2, C = G % 2;
-    static constexpr int B = P1 ? (I == 2 ? 1 : 0) : (I < 2 ? 0 : I < 4 ? 1 : I < 6 ? 2 : 3);   // X digit
-    static constexpr int A = P1 ? (I == 1 ? 1 : 0) : (I == 0 ? 2 : I == 1 ? 3 : I == 2 ? 1 : I == 3 ? 2 : I == 4 ? 0 : I == 5 ? 1 : 0);  // W digit
-    static constexpr int D = A + B;
-    static constexpr bool FIRST = (P1 ? (I <= 1) : (I <= 1)) && G == 0;  // first MFMA into its accumulator
-  };
-};
-
-// compile-time loop: f(integral_constant<int, 0>) … f(integral_constant<int, N − 1>)
-template <int N, int I = 0, class F>
-__device__ __forceinline__ void oz3_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    oz3_for<N, I + 1>(f);
-  }
-}
-// schedule groups of k_screen_oz3: MFMA J, then the vector instructions of its slot(s) (+1 for
-// one q01 merge over the first 16 MFMAs of phase 2)
-template <int NB, int J>
-struct Oz3Groups {
-  using S = S3<NB>;
-  static constexpr int SPM = 40 / S::NM;
-  static constexpr int NV = rt_slot_valu<J * SPM>() + (SPM == 2 ? rt_slot_valu<J * SPM + 1>() : 0) +
-                            (J >= S::NM1 && J < S::NM1 + 16 ? (SPM == 2 ? 2 : 1) : 0);
-  static __device__ __forceinline__ void emit() {
-    if constexpr (J < S::NM) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-      Oz3Groups<NB, J + 1>::emit();
-    }
-  }
-};
-
-template <int NB, int FILL>
-__global__ void __launch_bounds__(256, 1)
-k_screen_oz3(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
-             const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
-             double* __restrict__ partials) {
-  using S = S3<NB>;
-  using St = Oz3Step<NB>;
-  constexpr int KSO = S::KSO, U = S::U, TILE = S::TILE, SLOT = S::SLOT, NCP = S::NCP, RT = S::RT, WPR = S::WPR;
-  constexpr int PIECES = S::PIECES;
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int rt = wv % RT, wq = wv / RT;
-  const int n = lane & 31, gl = lane >> 5;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* tiles = smem;                             // [NBUF][U][SLOT]
-  uint8_t* scl = tiles + S::NBUF * U * SLOT;         // [NBUF][SCB]: per pair [2][16] fp32 scales
-  double* red = (double*)(scl + S::NBUF * S::SCB);   // [WPR][NCP][2]
-  const uint32_t b_begin = blockIdx.x * bpw;
-  const uint32_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
-  const uint32_t nb = b_begin < b_end ? b_end - b_begin : 0u;
-  const uint32_t nsteps = (nb + U - 1) / U;
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(xsl + (size_t)b_begin * TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * TILE)), RSRC_DW3);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
-  // DMA: wave w moves pieces 8w … 8w + 7 of the step's 32 (piece p of the step: block p / PIECES,
-  // digit-image KiB p mod PIECES; in LDS the step's pieces are contiguous); waves 4 − NSCALE … 3
-  // also one 256-B slice of the step's scales each (one dword per lane)
-  const uint32_t voff_x = (uint32_t)((S::PPW * wv / PIECES) * TILE + lane * 16);
-  const int sw = wv - (S::WAVES - S::NSCALE);  // ≥ 0: this wave's scale slice
-  const bool scale_wave = sw >= 0;
-  auto stage = [&](uint32_t step, int buf) {
-    uint8_t* dst = tiles + buf * U * SLOT + S::PPW * wv * 1024;
-#pragma unroll
-    for (int i = 0; i < S::PPW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rx, (lds_vptr2)(dst + i * 1024), 16,
-          (int)(voff_x + (i / PIECES) * TILE + (i % PIECES) * 1024 + step * (uint32_t)(U * TILE)), 0, 0, 0);
-    if (scale_wave)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB + sw * 256), 4,
-                                               (int)(sw * 256 + lane * 4 + step * (uint32_t)(U * 64)), 0, 0, 0);
-  };
-  // B operands: W rows 32rt + n, digits a ≤ 3, k-step s, chunk c: the 16 bytes of W-image lane
-  // (n mod 16) + 16(2c + gl) of row block 2rt + n/16 (the A operand's feature map)
-  v4i wb[4][KSO][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int s2 = 0; s2 < KSO; ++s2)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        wb[a][s2][c] = *(const v4i*)(wsl_g + (size_t)((((2 * rt + (n >> 4)) * SLICES + a) * 2 + s2) * 64 + (n & 15) +
-                                                      16 * (2 * c + gl)) * 16);
-  const double rowscale = __builtin_ldexp(wsc[rt * 32 + n], e0 - 8);  // 2^(f_i + E0 − 20)
-  const float cz = __builtin_fabsf(c32) * (float)rowscale;
-  // A operand of plane b, k-step s, chunk c in a staged pair: block (n >> 4) of the pair,
-  // image lane (n & 15) + 16(2c + gl)
-  const uint32_t a_lane = (uint32_t)((n >> 4) * SLOT + ((n & 15) + 16 * gl) * 16);
-  double l = 0.0, g = 0.0;
-  v16i q01p, r23p;  // the previous unit's merged diagonals (zero before the first: zero terms)
-#pragma unroll
-  for (int r = 0; r < 16; ++r) q01p[r] = r23p[r] = 0;
-  float sfp[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) sfp[r] = 0.f;
-  auto wait_step = [&]() {  // this wave's DMA of the NEXT step landed (counted), then every wave meets
-    if (scale_wave) asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  stage(0, 0);
-  stage(1, 1);
-  wait_step();
-  int buf = 0;
-  for (uint32_t k = 0; k < nsteps; ++k) {
-    stage(k + 2, buf == 0 ? 2 : buf - 1);  // (k + 2) mod 3; past the end: zeros, never read
-#pragma unroll
-    for (int j = 0; j < S::UPW; ++j) {
-      const int pp = wq + WPR * j;
-      const uint8_t* pb = tiles + (buf * U + 2 * pp) * SLOT + a_lane;
-      auto ra = [&](int b, int s2, int c) { return *(const v4i*)(pb + ((b * KSO + s2) * 64 + 32 * c) * 16); };
-      v16i acc[4];
-      RT3 t;
-      v4i x[4];
-      v16i q01;
-      auto op = [&](auto jc) {
-        constexpr int J = decltype(jc)::value;
-        using O = typename St::template Op<J>;
-        if constexpr (O::I == 0) {  // a new (k-step, chunk) group: its A operands
-#pragma unroll
-          for (int b = 0; b < (O::P1 ? 2 : 4); ++b) x[b] = ra(b, O::SS, O::C);
-        }
-        if constexpr (O::FIRST) acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], v16i{});
-        else acc[O::D] = mfma32_i8(x[O::B], wb[O::A][O::SS][O::C], acc[O::D]);
-        if constexpr (J == S::NM1 - 1) {  // D ≤ 1 complete: merge (spread by the schedule groups)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) q01[r] = acc[0][r] * 256 + acc[1][r];
-        }
-        if constexpr (FILL > 0) {
-          rt_slot<J * St::SPM>(t, q01p, r23p, sfp, cz, l, g);
-          if constexpr (St::SPM == 2) rt_slot<J * St::SPM + 1>(t, q01p, r23p, sfp, cz, l, g);
-        }
-      };
-      oz3_for<S::NM>(op);
-      if constexpr (FILL == 0) row_terms16(q01p, r23p, sfp, cz, l, g);
-      if constexpr (FILL > 0) Oz3Groups<NB, 0>::emit();
-      asm volatile("" ::"v"(l), "v"(g));  // the row terms stay in this unit (not sunk past the wait)
-      __builtin_amdgcn_sched_barrier(0);  // each unit its own scheduling region
-#pragma unroll
-      for (int r = 0; r < 16; ++r) r23p[r] = acc[2][r] * 256 + acc[3][r];
-      q01p = q01;
-      // this unit's scales: pair pp, lane group gl — 16 floats (the layout of k_build_xsf3)
-      const float* sp = (const float*)(scl + buf * S::SCB) + pp * 32 + gl * 16;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const f4v tv = *(const f4v*)(sp + 4 * v);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sfp[4 * v + i] = tv[i];
-      }
-    }
-    wait_step();
-    buf = buf == 2 ? 0 : buf + 1;
-  }
-  row_terms16(q01p, r23p, sfp, cz, l, g);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  double rs_y = l * rowscale;
-  double rs_ll = __builtin_fma(g, ln2_alpha, rs_y);
-  rs_ll += __shfl_xor(rs_ll, 32);
-  rs_y += __shfl_xor(rs_y, 32);
-  if (gl == 0) {
-    red[(wq * NCP + rt * 32 + n) * 2 + 0] = rs_ll;
-    red[(wq * NCP + rt * 32 + n) * 2 + 1] = rs_y;
-  }
-  __syncthreads();
-  double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
-  for (int e = threadIdx.x; e < 2 * NCP; e += 256) {
-    const int c = e / NCP, row = e % NCP;
-    double v = 0.0;
-#pragma unroll
-    for (int q = 0; q < WPR; ++q) v += red[(q * NCP + row) * 2 + c];
-    out[e] = v;
-  }
-}
-
-// xsf3[32·p + 16·gl + r] = 2^(e_t − E0) for the sample of output row m = 8(r/4) + 4gl + (r mod 4)
-// of block pair p: block 2p + m/16, image row m mod 16, sample σ(m mod 16) (k_screen_oz3's map)
-__global__ void __launch_bounds__(256) k_build_xsf3(const double* __restrict__ xsc, uint64_t n, int e0,
-                                                    float* __restrict__ xsf) {
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t p = i >> 5;
-    const int gl = (int)(i >> 4) & 1, r = (int)i & 15;
-    const int m = 8 * (r >> 2) + 4 * gl + (r & 3);
-    const int m16 = m & 15, sig = (m16 >> 2) + 4 * (m16 & 3);
-    xsf[i] = (float)__builtin_ldexp(xsc[(2 * p + (m >> 4)) * 16 + sig], -e0);
-  }
-}
-
-template <int NB, int FILL>
-hipError_t launch3_fill(const Screen2Args& a, hipStream_t stream) {
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz3<NB, FILL>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, S3<NB>::LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  k_screen_oz3<NB, FILL><<<a.nwg, 256, S3<NB>::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
-                                                                a.bpw, a.n_blocks, a.partials);
-  return hipGetLastError();
-}
-// PICARD_SCREEN2_FILL=0: the row terms in the compiler's order; otherwise spread over the MFMAs
-template <int NB>
-hipError_t launch3(const Screen2Args& a, hipStream_t stream) {
-  return fill_knob() == 0 ? launch3_fill<NB, 0>(a, stream) : launch3_fill<NB, 1>(a, stream);
-}
 }  // namespace
 
 int screen2_blocks_per_step(int nb) { return 8 / nb; }
-int screen3_blocks_per_step(int nb) { return nb == 8 ? S3<8>::U : S3<4>::U; }
-uint64_t screen3_lds_bytes(int nb) { return nb == 8 ? S3<8>::LDS : S3<4>::LDS; }
-hipError_t screen3_launch(int nb, const Screen2Args& a, hipStream_t stream) {
-  return nb == 8 ? launch3<8>(a, stream) : launch3<4>(a, stream);
-}
-hipError_t screen3_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream) {
-  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-  k_build_xsf3<<<grid ? grid : 1, 256, 0, stream>>>(xsc, n, e0, xsf);
-  return hipGetLastError();
-}
 uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }
 
 hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream) {

@@ -27,11 +27,5 @@ int screen2_blocks_per_step(int nb);   // 16-sample blocks per loop step (NB = 8
 uint64_t screen2_tile_bytes(int nb);   // bytes of one block's digit image
 hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream);
 hipError_t screen2_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream);
-// k_screen_oz3 (NB = 8 and 4, v_mfma_i32_32x32x32_i8): 4 (NB = 8) or 8 (NB = 4) blocks per step,
-// one workgroup per CU; its scales in the k_build_xsf3 layout (n a multiple of 32 samples)
-int screen3_blocks_per_step(int nb);
-uint64_t screen3_lds_bytes(int nb);
-hipError_t screen3_launch(int nb, const Screen2Args& a, hipStream_t stream);
-hipError_t screen3_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream);
 
 }  // namespace pcamd
