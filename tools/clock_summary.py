@@ -6,6 +6,9 @@ import csv
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from knames import kname  # noqa: E402
+
 d = sys.argv[1]
 dur = {}
 for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
@@ -14,7 +17,7 @@ per = collections.defaultdict(dict)
 names = {}
 for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
     k = r["Dispatch_Id"]
-    names[k] = r["Kernel_Name"].split("(")[0]
+    names[k] = kname(r["Kernel_Name"])
     per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for k, c in per.items():

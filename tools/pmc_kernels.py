@@ -19,6 +19,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from knames import kname  # noqa: E402
+
 
 def load(d):
     dur = {}
@@ -31,7 +34,7 @@ def load(d):
     cp = os.path.join(d, "run_counter_collection.csv")
     for r in csv.DictReader(open(cp)):
         k = r["Dispatch_Id"]
-        names[k] = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pcamd::", "")
+        names[k] = kname(r["Kernel_Name"])
         per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return dur, per, names
 

@@ -10,6 +10,7 @@ import csv
 import json
 import sys
 from collections import defaultdict
+from knames import kname
 
 KERNELS = {"k_eval_fused": lambda n, t: 8.0 * n * t, "k_eval_loss": lambda n, t: 8.0 * n * t,
            "k_screen_oz": lambda n, t: 8.0 * n * t}
@@ -30,7 +31,7 @@ def main():
                                           (short == "k_eval_fused" and "k_eval_fused_ws<0," in name) or
                                           (short == "k_eval_loss" and ("k_eval_loss2<0, false," in name or
                                                                        "k_eval_loss_oz<0, false," in name))):
-                        vals[(short, name.split("(")[0])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                        vals[(short, kname(name))][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {"n": n, "t_local": t_local, "sources": sys.argv[4:], "kernels": {}}
     for short in KERNELS:
         cands = [k for k in vals if k[0] == short and vals[k]["FETCH_SIZE"]]

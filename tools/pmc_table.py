@@ -9,13 +9,16 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from knames import kname  # noqa: E402
+
 
 def load(path):
     agg = defaultdict(lambda: defaultdict(list))
     if not os.path.exists(path):
         return agg
     for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pcamd::", "")][r["Counter_Name"]].append(
+        agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(
             float(r["Counter_Value"]))
     return agg
 
@@ -27,7 +30,7 @@ def main():
     wri = load(os.path.join(d, pre + "_write", "run_counter_collection.csv"))
     dur = defaultdict(list)
     for r in csv.DictReader(open(os.path.join(d, pre + "_clock", "run_kernel_trace.csv"))):
-        dur[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pcamd::", "")].append(
+        dur[kname(r["Kernel_Name"])].append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     print("%-58s %5s %9s %5s %6s %9s %9s %9s %10s" % ("kernel", "n", "ms", "GHz", "mfma", "VALU", "MFMA", "LDS",
                                                     "HBM GB"))

@@ -7,17 +7,8 @@ import os
 import sys
 from collections import defaultdict
 
-
-def kname(raw):
-    """Kernel name without return type, namespaces or parameter list (template arguments kept)."""
-    k = raw.replace("(anonymous namespace)::", "").replace("pcamd::", "").replace("void ", "")
-    depth = 0
-    for i, ch in enumerate(k):
-        depth += ch == "<"
-        depth -= ch == ">"
-        if ch == "(" and depth == 0:
-            return k[:i].strip()
-    return k.strip()
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from knames import kname  # noqa: E402
 
 
 def main():
