@@ -1,14 +1,14 @@
-# usage: bash tools/gpu_jade2.sh TAG — JADE tests, C5 with one-wave and four-wave sweep workgroups
-# (PICARD_JADE_THREADS), then the kernel trace of the default (rocprofv3's exit crash tolerated, last)
+# usage: bash tools/gpu_jade2.sh TAG — JADE tests, C5 twice with the warm-start trace, then the kernel
+# trace of C5
 TAG=$1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_jade.py tests/test_gpu_parity.py -k "jade" -x -q --timeout 200 --timeout-method thread \
   > gpurun_out/pytest_jade_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_jade_$TAG.log; exit 1; }
 tail -2 gpurun_out/pytest_jade_$TAG.log
-for th in 256 256; do
-  PICARD_JADE_THREADS=$th PICARD_TRACE=1 timeout -k 10 200 python3 tools/run_configs.py C5 > gpurun_out/c5_$TAG.$th.json 2> gpurun_out/c5_$TAG.$th.log || exit 1
-  echo "threads $th: $(grep 'jade:' gpurun_out/c5_$TAG.$th.log)"
+for i in 1 2; do
+  PICARD_TRACE=1 timeout -k 10 200 python3 tools/run_configs.py C5 > gpurun_out/c5_$TAG.$i.json 2> gpurun_out/c5_$TAG.$i.log || exit 1
+  echo "run $i: $(grep 'jade:' gpurun_out/c5_$TAG.$i.log)"
 done
 O=gpurun_out/prof_$TAG
 mkdir -p $O
