@@ -7,7 +7,7 @@
 //     cycles, and vector instructions co-issue beside it only from the SAME wave (an MFMA wave
 //     beside a VALU wave runs serialised: tools/microbench/agpr_coexec.hip). So each wave
 //     interleaves the row terms of its previous step between the MFMAs of its current step
-//     (sched_group_barrier: one MFMA, then two vector instructions), instead of 20 MFMAs
+//     (sched_group_barrier: one MFMA, then one vector instruction), instead of 20 MFMAs
 //     followed by a block of VALU;
 //   * fewer vector instructions per element: the sample scale 2^(e_t − E0) comes in fp32 from
 //     a per-image array (k_build_xsf, 4 B per sample, laid out so one ds_read_b128 gives a
@@ -247,11 +247,13 @@ hipError_t launch_fill(const Screen2Args& a, hipStream_t stream) {
                                                           a.n_blocks, a.partials);
   return hipGetLastError();
 }
-// PICARD_SCREEN2_FILL (measurement knob): vector instructions per MFMA gap, 0 = compiler order
+// PICARD_SCREEN2_FILL (measurement knob): vector instructions per MFMA gap, 0 = compiler order.
+// Default 1: (128, 2e7) 3.20–3.26 ms against 3.29–3.31 for 2 and 3.30–3.32 for 0, alternating
+// on one box (profiles/r04_e/screen_fill_ab.txt)
 int fill_knob() {
   static const int v = [] {
     const char* e = std::getenv("PICARD_SCREEN2_FILL");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : 1;
   }();
   return v;
 }
@@ -259,12 +261,10 @@ template <int NB>
 hipError_t launch(const Screen2Args& a, hipStream_t stream) {
   switch (fill_knob()) {
     case 0: return launch_fill<NB, 0>(a, stream);
-    case 1: return launch_fill<NB, 1>(a, stream);
-    case 3: return launch_fill<NB, 3>(a, stream);
-    default: return launch_fill<NB, 2>(a, stream);
+    case 2: return launch_fill<NB, 2>(a, stream);
+    default: return launch_fill<NB, 1>(a, stream);
   }
 }
-
 
 }  // namespace
 
