@@ -379,6 +379,14 @@ uint64_t pc_ctx_int8_passes(const pc_ctx* ctx);
  * nc ≤ 64 or above 128, cube, α ≤ 0). */
 int pc_ctx_eval_loss_screen(pc_ctx* ctx, const double* w, uint64_t nc, const double* mu, pc_density density,
                             double* ll_out, double* bound_out, char* err, size_t errlen);
+/* Two tries' screens in ONE pass (w1, w2: nc × n_features each): ll1/bound1 and ll2/bound2 are
+ * what pc_ctx_eval_loss_screen returns for w1 and for w2 alone (the same arithmetic per W; the
+ * solver pairs the screened tries of a non-descent search with it). tanh, the
+ * default D ≤ 3 fp32 screen only; PC_ERR_UNSUPPORTED where it does not apply (or with
+ * PICARD_SCREEN_PAIRS=0). With a communicator, collective like pc_ctx_eval. */
+int pc_ctx_eval_loss_screen2(pc_ctx* ctx, const double* w1, const double* w2, uint64_t nc, const double* mu,
+                             pc_density density, double* ll1, double* bound1, double* ll2, double* bound2,
+                             char* err, size_t errlen);
 /* line-search screen passes since the last reset: summed HIP-event kernel ms and count */
 void pc_ctx_screen_stats(pc_ctx* ctx, double* kernel_ms, uint64_t* n_launches, int32_t reset);
 /* Exhaustive accuracy of the fp32 instructions the line-search screen evaluates its

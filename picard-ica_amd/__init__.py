@@ -204,6 +204,7 @@ def _load():
         "pc_ctx_int8_passes": (u64, [vp]),
         "pc_ctx_screen_stats": (None, [vp, d, P(u64), i32]),
         "pc_ctx_eval_loss_screen": (C.c_int, [vp, d, u64, d, _Density, d, d, cp, sz]),
+        "pc_ctx_eval_loss_screen2": (C.c_int, [vp, d, d, u64, d, _Density, d, d, d, d, cp, sz]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -231,7 +232,7 @@ EXPORTED = [
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_solver_timing", "pc_solver_setup_timing", "pc_fit_with_evaluator",
 ]
 
@@ -747,6 +748,20 @@ class DeviceContext:
         _raise(lib.pc_ctx_eval_loss_screen(self.h, _ptr(w), nc, _ptr(mu_a) if mu_a is not None else None,
                                            density._c(), _ptr(ll), _ptr(bnd), err, len(err)), err)
         return ll, bnd
+
+    def eval_loss_screen2(self, w1, w2, mu=None, density: DensityType = DensityType()):
+        """pc_ctx_eval_loss_screen2: two tries in one pass → ((Σℓ, bound) of w1, (Σℓ, bound) of w2),
+        each as eval_loss_screen gives it for that W alone."""
+        w1, w2 = _c64(w1), _c64(w2)
+        nc = w1.shape[0]
+        if w2.shape != w1.shape:
+            raise InvalidDimensions("eval_loss_screen2: w1 and w2 differ in shape")
+        mu_a = _c64(mu) if mu is not None else None
+        out = [np.empty(nc) for _ in range(4)]
+        err = _errbuf()
+        _raise(lib.pc_ctx_eval_loss_screen2(self.h, _ptr(w1), _ptr(w2), nc, _ptr(mu_a) if mu_a is not None else None,
+                                            density._c(), *[_ptr(o) for o in out], err, len(err)), err)
+        return (out[0], out[1]), (out[2], out[3])
 
     def screen_stats(self, reset: bool = False):
         """pc_ctx_screen_stats: (Σ screen-pass kernel ms, screen passes) since the last reset."""

@@ -508,6 +508,15 @@ int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const doubl
   });
 }
 
+int pc_ctx_eval_loss_screen2(pc_ctx* c, const double* w1, const double* w2, uint64_t nc, const double* mu,
+                             pc_density density, double* ll1, double* bound1, double* ll2, double* bound2,
+                             char* err, size_t errlen) {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
+    if (!c->ev->eval_loss_screen2(w1, w2, nc, mu, density, ll1, bound1, ll2, bound2))
+      throw unsupported("no paired line-search screen for this shape / density");
+  });
+}
+
 void pc_ctx_screen_stats(pc_ctx* c, double* ms, uint64_t* n, int32_t reset) {
   device_ctx_screen_stats(c->ev.get(), ms, n, reset);
 }

@@ -3718,6 +3718,23 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + img_bytes, hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
+  // two tries' W for the paired screen: w1 in row blocks 0 … NB − 1, w2 in NB … 2·NB − 1 (row
+  // scales 0 … and 16·NB …), the layout k_screen_oz2<NB, ·, 2> reads
+  void upload_wsl_pair(const double* w1, const double* w2, size_t nc, int nb) {
+    alloc_wsl();
+    if (nc > (size_t)16 * nb) throw computation_error("paired W image: nc > 16·NB");
+    const int ksw = wsl_ksw();
+    const size_t half = (size_t)nb * OZ_SLICES * ksw * 64 * 16;
+    double* sc = (double*)pin_acquire(pin_wsl_, WSC_BYTES + WSL_IMG_MAX);
+    uint8_t* img = (uint8_t*)sc + WSC_BYTES;
+    std::memset(img, 0, 2 * half);
+    for (int i = 0; i < 512; ++i) sc[i] = 0x1p-12;
+    oz_split_rows(w1, nc, nf, img, sc, ksw);
+    oz_split_rows(w2, nc, nf, img + half, sc + 16 * nb, ksw);
+    wsl_nc_ = 0;  // the image no longer holds a single W
+    HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + 2 * half, hipMemcpyHostToDevice, stream));
+    pin_release(pin_wsl_);
+  }
   // NB = 8 (64 < nc ≤ 128) or NB = 4 (32 < nc ≤ 64, nf ≤ 64; partition in 32-sample blocks,
   // that of k_eval_fused<4> / k_eval_loss<4>)
   template <int D, bool Q, int DMAX = OZ_SLICES - 1, bool F32L = false, int NB = 8>
@@ -3834,6 +3851,116 @@ struct DeviceCtx : Evaluator {
   bool eval_loss_screen_fine(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
                              double* bound_out) override {
     return screen_dmax_ < 4 && screen_at(4, w, nc, mu, d, ll_out, bound_out);
+  }
+  // W row exponents (the kernels' f_i: 2^f_i > max_k |W_ik|; 0 for a zero row), and whether
+  // the fp32 screen's scales 2^(f_i+e_t−20) all stay normal fp32 with room (see screen_at)
+  void screen_row_exps(const double* w, size_t nc, std::vector<int>& fexp, bool& f32_ok) const {
+    fexp.assign(nc, 0);
+    for (size_t i = 0; i < nc; ++i) {
+      double mx = 0.0;
+      for (size_t k = 0; k < nf; ++k) {
+        const double f = std::fabs(w[i * nf + k]);
+        mx = f > mx ? f : mx;  // = fmax: a NaN weight is skipped, as fmax skips it
+      }
+      if (mx > 0.0) {
+        (void)std::frexp(mx, &fexp[i]);
+        if (fexp[i] - 20 + xsc_emin_ < -100 || fexp[i] - 20 + xsc_emax_ > 99) f32_ok = false;
+      }
+    }
+  }
+  // this rank's part of the bound per row (screen_at's tail and fp32 terms)
+  void screen_rank_bound(int dmax, const std::vector<int>& fexp, size_t nc, pc_density d, bool f32l, double* bnd) const {
+    auto pm = [](int dd) {  // Σ_{a+b=dd} |d_a|max·|d_b|max per feature
+      double v = 0.0;
+      for (int a = 0; a < OZ_SLICES; ++a) {
+        const int b = dd - a;
+        if (b >= 0 && b < OZ_SLICES) v += (a == 0 ? 65.0 : 128.0) * (b == 0 ? 65.0 : 128.0);
+      }
+      return v;
+    };
+    double bsum = 0.0;
+    for (int dd = dmax + 1; dd <= OZ_SLICES - 1; ++dd) bsum += std::ldexp(pm(dd), -8 * dd);  // exact stage: D ≤ 6
+    if (f32l) bsum += std::ldexp(256.0 * pm(2) + pm(3) + pm(4) / 256.0, -46) * (1.0 + 1e-6);
+    const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
+    const double tail = (double)nf * bsum * xsc_sum_ * lip;
+    for (size_t i = 0; i < nc; ++i) {
+      bnd[i] = std::ldexp(tail, fexp[i] - 12) * (1.0 + 1e-12);
+      if (f32l) bnd[i] += (double)(ldx / 4) * screen_f32_block_bound(d.alpha);
+    }
+  }
+  // PICARD_SCREEN_PAIRS=0: no paired screens (the solver screens tries one by one)
+  const bool screen_pairs_ = !(std::getenv("PICARD_SCREEN_PAIRS") && std::atoi(std::getenv("PICARD_SCREEN_PAIRS")) == 0);
+  int screen_pair_agreed_ = 0;
+  // the sample-exponent window every rank's image must lie in for the paired screen: the fp32
+  // range test then depends on W alone (rank-identical), so every rank takes the same branch
+  static constexpr int PAIR_EMIN = -40, PAIR_EMAX = 40;
+  // Two tries in one pass (k_screen_oz2<NB, ·, 2>): the tanh fp32 D ≤ 3 screen only. A paired
+  // and a single screen issue different all-reduces, so with a communicator the ranks agree once
+  // that each holds the digit image and its fp32 scales with sample exponents inside
+  // [PAIR_EMIN, PAIR_EMAX]; the per-call test (both W's row exponents against that window) is on
+  // rank-identical data. Each try's rows are those of screen_at for that W alone: the same
+  // kernel arithmetic per W, the same bound terms.
+  bool eval_loss_screen2(const double* w1, const double* w2, size_t nc, const double* mu, pc_density d, double* ll1,
+                         double* bnd1, double* ll2, double* bnd2) override {
+    if (!screen_pairs_ || screen_dmax_ != 3 || !screen_nows_ || !screen_v2_ || !screen_f32_) return false;
+    if (y_stage_ != 0 || !oz_any(nc) || !(d.alpha > 0.0) || d.kind != DENS_TANH) return false;
+    std::vector<int> f1, f2;
+    bool w_ok = true;
+    screen_row_exps(w1, nc, f1, w_ok);
+    screen_row_exps(w2, nc, f2, w_ok);
+    for (size_t i = 0; i < nc && w_ok; ++i)
+      w_ok = f1[i] - 20 + PAIR_EMIN >= -100 && f1[i] - 20 + PAIR_EMAX <= 99 && f2[i] - 20 + PAIR_EMIN >= -100 &&
+             f2[i] - 20 + PAIR_EMAX <= 99;
+    if (!w_ok) return false;  // rank-identical
+    const bool nb4 = oz4_shape(nc);
+    const int nb = nb4 ? 4 : 8;
+    HIP_OK(hipSetDevice(device));
+    const double* dmu = resident_mu(mu);
+    double* st_rows = ensure(d_stats, cap_stats, 6 * nc);  // per try [Σℓ | Σ|ỹ| | bound]
+    {
+      uint64_t bpw0;
+      const int nwg0 = partition(nb4 ? (n_local_ + 31) / 32 : (n_local_ + 15) / 16, &bpw0);
+      ensure(d_part, cap_part, (size_t)std::max(nwg0, 2 * n_cu) * 2 * 2 * (nb4 ? 64 : 128));
+    }
+    bool ok = dmu == nullptr && ensure_xsl() && ensure_xsf() && xsc_range_ok_ && xsc_emin_ >= PAIR_EMIN &&
+              xsc_emax_ <= PAIR_EMAX;
+    if (coll_) ok = agree_once(screen_pair_agreed_, ok, "the paired line-search screen");
+    if (!ok) return false;
+    upload_wsl_pair(w1, w2, nc, nb);
+    d_wsl_ready_ = false;  // the image holds two W's: no completion may reuse it
+    kept_nc_pending = nc;
+    HIP_OK(hipEventRecord(ev[0], stream));
+    double* direct = direct_acquire(6 * nc);
+    if (direct) st_rows = direct;
+    const bool launched = nb4 ? launch_screen_oz2<4>(d.alpha, st_rows, 2) : launch_screen_oz2<8>(d.alpha, st_rows, 2);
+    if (!launched) throw computation_error("paired screen: launch geometry out of range after the agreement");
+    double* bnd = direct ? direct : (double*)pin_acquire(pin_in_, 6 * nc * sizeof(double));
+    screen_rank_bound(3, f1, nc, d, true, bnd + 2 * nc);
+    screen_rank_bound(3, f2, nc, d, true, bnd + 5 * nc);
+    std::vector<double> tmp(6 * nc);
+    const double* staged = direct;
+    if (direct) {
+      pin_release(pin_direct_);  // the kernel writes rows 0–1 of each try, the host row 2
+    } else {
+      HIP_OK(hipMemcpyAsync(st_rows + 2 * nc, bnd + 2 * nc, nc * sizeof(double), hipMemcpyHostToDevice, stream));
+      HIP_OK(hipMemcpyAsync(st_rows + 5 * nc, bnd + 5 * nc, nc * sizeof(double), hipMemcpyHostToDevice, stream));
+      pin_release(pin_in_);
+      allreduce(st_rows, 6 * nc, "screen pair");
+      staged = d2h_enqueue(st_rows, 6 * nc);
+    }
+    finish_timing(true, 4);
+    copy_out(tmp.data(), staged, 6 * nc);
+    const double kappa1 = 0x1p-22 * 1.0001;
+    for (int t = 0; t < 2; ++t) {
+      const double* r = tmp.data() + (size_t)t * 3 * nc;
+      double* llo = t ? ll2 : ll1;
+      double* bo = t ? bnd2 : bnd1;
+      for (size_t i = 0; i < nc; ++i) {
+        llo[i] = r[i];
+        bo[i] = r[2 * nc + i] + kappa1 * std::fabs(r[nc + i]) + 1e-10 * std::fabs(r[i]);
+      }
+    }
+    return true;
   }
   bool screen_at(int dmax, const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
                  double* bound_out) {
@@ -3955,7 +4082,7 @@ struct DeviceCtx : Evaluator {
   // schedule; PICARD_SCREEN_V2=0 keeps k_screen_oz. false: not available here.
   bool screen_v2_ = !(std::getenv("PICARD_SCREEN_V2") && std::atoi(std::getenv("PICARD_SCREEN_V2")) == 0);
   template <int NB>
-  bool launch_screen_oz2(double alpha, double* st_rows) {
+  bool launch_screen_oz2(double alpha, double* st_rows, int nw = 1) {
     constexpr int NCP = 16 * NB;
     const int U = screen2_blocks_per_step(NB);
     const uint64_t n_blocks = (n_local_ + 15) / 16;
@@ -3966,7 +4093,7 @@ struct DeviceCtx : Evaluator {
     // 32-bit buffer offsets within a workgroup's range (and the kernel's 32-bit block counts)
     if ((bpw + 2 * (uint64_t)U) * screen2_tile_bytes(NB) >= (1ull << 31) || n_blocks >= (1ull << 32)) return false;
     if (!ensure_xsf()) return false;
-    double* part = ensure(d_part, cap_part, (size_t)nwg * 2 * NCP);
+    double* part = ensure(d_part, cap_part, (size_t)nwg * nw * 2 * NCP);
     if (!xsl_valid_ || !d_xsl) throw computation_error("int8 digit image released while a pass was set up");
     if (oz_kso() != (NB == 8 ? 2 : 1)) throw computation_error("int8 digit image of another layout");
     Screen2Args a;
@@ -3975,12 +4102,17 @@ struct DeviceCtx : Evaluator {
     a.e0 = xsf_e0_;
     a.ln2_alpha = fm::LN2 / alpha;
     a.bpw = (uint32_t)bpw; a.n_blocks = (uint32_t)n_blocks; a.nwg = nwg; a.partials = part;
+    a.nw = nw;
     HIP_OK(hipEventRecord(ev[1], stream));
     HIP_OK(screen2_launch(NB, a, stream));
     HIP_OK(hipEventRecord(ev[2], stream));
-    k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
-        part, nwg, 2 * NCP, 0, NCP, (int)kept_nc_pending, 2, st_rows, DENS_TANH, alpha, (double)n_local_, 1);
-    HIP_OK(hipGetLastError());
+    // try w's rows into st_rows + w·3·nc ([Σℓ | Σ|ỹ|], the bound row is the host's)
+    for (int w = 0; w < nw; ++w) {
+      k_reduce_rows<<<(2 * (int)kept_nc_pending + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(
+          part, nwg, (size_t)nw * 2 * NCP, (size_t)w * 2 * NCP, NCP, (int)kept_nc_pending, 2,
+          st_rows + (size_t)w * 3 * kept_nc_pending, DENS_TANH, alpha, (double)n_local_, 1);
+      HIP_OK(hipGetLastError());
+    }
     ++n_int8_passes_;
     ++n_screen_passes_;
     return true;

@@ -107,6 +107,14 @@ class Evaluator {
     (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
     return false;
   }
+  // Two tries' screens in one pass (w1, w2: the same shape): each try's [Σℓ, bound] exactly as
+  // eval_loss_screen gives it for that W alone. false = not available here (the caller then
+  // screens the tries one by one).
+  virtual bool eval_loss_screen2(const double* w1, const double* w2, size_t nc, const double* mu, pc_density d,
+                                 double* ll1, double* bound1, double* ll2, double* bound2) {
+    (void)w1; (void)w2; (void)nc; (void)mu; (void)d; (void)ll1; (void)bound1; (void)ll2; (void)bound2;
+    return false;
+  }
   // Non-ortho line search: Σℓ and Σy² of Y_j = (W + α_j·Z)·(X−μ) for every α_j
   // in one pass (ll_out, y2_out: [na][nc]). false = not supported here.
   virtual bool eval_loss_multi(const double* w, const double* z, size_t nc, const double* mu, pc_density d,

@@ -508,6 +508,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
   LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false, false};
+  // a paired screen's second try (Evaluator::eval_loss_screen2): its rows, for try pair_k
+  std::vector<double> pair_ll, pair_bnd;
+  size_t pair_k = tries;
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
@@ -684,11 +687,45 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       const Mat wt = matmul(r.w, P_);
       ev_->want_y2 = false;
       const double t0 = now_ms();
-      if (ev_->eval_loss_screen(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(), bnd.data())) {
-        screened = true;
-        screen_seen_ = true;
+      const double* mu = has_mu_ ? mu_.data() : nullptr;
+      bool got = false;
+      const char* via = "";
+      if (pair_k == k) {  // screened with the previous try's pass
+        via = " (paired)";
+        ll = pair_ll;
+        bnd = pair_bnd;
+        pair_k = tries;
+        got = true;
+      } else if (first_loss_only && pairs_ok_ && k + 1 < tries && ahead_ &&
+                 !(ls_curv_ > 0.0 && curvature_lower_bound(alpha / 2.0) > ls_slack_)) {
+        // Schedule only: a non-descent direction (⟨g, D⟩ ≥ 0) almost surely fails every try,
+        // and its next try will be screened too (not rejected by curvature), so both tries go
+        // in one pass — half the bytes per try for a screen whose clock the memory side's power
+        // holds down. Each try's rows are those of its own screen (the same
+        // arithmetic per W), so every decision is unchanged.
+        const Mat wt2 = matmul(ahead_->get(k + 1, &ahead_wait_ms_), P_);
+        pair_ll.assign(n, 0.0);
+        pair_bnd.assign(n, 0.0);
+        if (ev_->eval_loss_screen2(wt.data(), wt2.data(), n, mu, cfg_.density, ll.data(), bnd.data(), pair_ll.data(),
+                                   pair_bnd.data())) {
+          pair_k = k + 1;
+          ++screen_pairs_;
+          via = " (pair)";
+          got = true;
+          eval_ms_ += now_ms() - t0;
+          ++screen_passes_;
+        } else {
+          pairs_ok_ = false;  // not available here: single screens from now on
+        }
+      }
+      if (!got && ev_->eval_loss_screen(wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) {
+        got = true;
         eval_ms_ += now_ms() - t0;
         ++screen_passes_;
+      }
+      if (got) {
+        screened = true;
+        screen_seen_ = true;
         double lo = 0.0, eb = 0.0;
         for (size_t i = 0; i < n; ++i) {
           lo += (signs_[i] * ll[i] - std::fabs(signs_[i]) * bnd[i]) / (double)T_;
@@ -696,14 +733,13 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         }
         rejected = !(lo < current_loss_);  // exact loss ≥ lo ≥ current: the try fails
         if (trace_)
-          std::fprintf(stderr, "[picard-screen] try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", k + 1, alpha,
-                       lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact");
+          std::fprintf(stderr, "[picard-screen] try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s%s\n", k + 1, alpha,
+                       lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact", via);
         // undecided, but the estimate lies above the current loss (a likely rejection): the
         // finer screen first, when the evaluator has one, before the full pass. Its inputs
         // are the reduced statistics, so every rank takes the same branch.
         if (!rejected && lo + eb > current_loss_ &&
-            ev_->eval_loss_screen_fine(wt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density, ll.data(),
-                                       bnd.data())) {
+            ev_->eval_loss_screen_fine(wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) {
           ++screen_passes_;
           lo = 0.0;
           eb = 0.0;
@@ -880,11 +916,11 @@ bool Solver::step() {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
                  " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f map_wait_ms %.3f screens %llu rejected %llu"
-                 " curv_skips %llu\n",
+                 " curv_skips %llu screen_pairs %llu\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
                  res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_, ahead_wait_ms_ - wait_t0,
                  (unsigned long long)screen_passes_, (unsigned long long)screen_rejects_,
-                 (unsigned long long)curv_skips_);
+                 (unsigned long long)curv_skips_, (unsigned long long)screen_pairs_);
   }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;

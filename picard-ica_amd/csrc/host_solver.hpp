@@ -117,6 +117,8 @@ class Solver {
   uint64_t screen_passes_ = 0, screen_rejects_ = 0;  // line-search tries screened / rejected by the screen
   bool screen_ok_ = true;  // false once the evaluator declined a screen (then never asked again)
   bool screen_seen_ = false;  // a screen has run (the evaluator screens: tries need not all be exact)
+  bool pairs_ok_ = true;      // false once the evaluator declined a paired screen
+  uint64_t screen_pairs_ = 0;  // paired screens (two tries per pass)
   // Curvature rejection of orthogonal tries (Solver::set_curvature): C1 = P·Gram·Pᵀ/T, the
   // whitened covariance; per search a lower bound on L'(0), a bound on |L''| along
   // expm(αD)·W and the rounding slack; ls_curv_ = 0 disables

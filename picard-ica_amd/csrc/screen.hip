@@ -79,12 +79,18 @@ struct S2 {
   static constexpr int SLOT = PL * KSO * 1024;         // LDS bytes of one block's planes
   static constexpr int PIECES = PL * KSO;              // 1-KiB pieces per block (U·PIECES = 8)
   static constexpr int NBUF = 3, SCB = 256;
-  static constexpr int LDS = NBUF * U * SLOT + NBUF * SCB + U * NCP * 2 * 8;
+  template <int NW>
+  static constexpr int lds() { return NBUF * U * SLOT + NBUF * SCB + NW * U * NCP * 2 * 8; }
 };
 
-// FILL: vector instructions scheduled after each MFMA (0: no schedule groups, the compiler's order)
-template <int NB, int FILL>
-__global__ void __launch_bounds__(512, 2)
+// FILL: vector instructions scheduled after each MFMA (0: no schedule groups, the compiler's order).
+// NW = 2: two tries at once (the W image's row blocks NB … 2·NB − 1 and row scales 16·NB … hold
+// the second W): every X operand read and staged once for both, each W's row terms in the
+// arithmetic and order of NW = 1 (so each W's sums are bit-identical to its own screen), partials
+// [nwg][NW][2·NCP]. Half the HBM bytes per try: the screen's clock is held down by the memory
+// side's power (profiles/r04_e/screen_clock.txt), and two tries per pass relieve it.
+template <int NB, int FILL, int NW>
+__global__ void __launch_bounds__(512, NW == 1 ? 2 : 1)
 k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
              const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
              double* __restrict__ partials) {
@@ -132,19 +138,29 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
     else asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  v4i wsl[4][KSO];
+  v4i wsl[NW][4][KSO];
+  double rowscale[NW];
+  float cz[NW];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int w = 0; w < NW; ++w) {
+    const int rb = yi + NB * w;  // this try's row block in the W image
 #pragma unroll
-    for (int s = 0; s < KSO; ++s)
-      wsl[a][s] = *(const v4i*)(wsl_g + (size_t)(((yi * SLICES + a) * 2 + s) * 64 + lane) * 16);
-  const double rowscale = __builtin_ldexp(wsc[yi * 16 + lr], e0 - 8);  // 2^(f_i + E0 − 20)
-  const float cz = __builtin_fabsf(c32) * (float)rowscale;               // exact: a power-of-2 scaling
-  double l = 0.0, g = 0.0;
-  v4i acc[2][4];
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int s = 0; s < KSO; ++s)
+        wsl[w][a][s] = *(const v4i*)(wsl_g + (size_t)(((rb * SLICES + a) * 2 + s) * 64 + lane) * 16);
+    rowscale[w] = __builtin_ldexp(wsc[rb * 16 + lr], e0 - 8);  // 2^(f_i + E0 − 20)
+    cz[w] = __builtin_fabsf(c32) * (float)rowscale[w];          // exact: a power-of-2 scaling
+  }
+  double l[NW], g[NW];
+  v4i acc[2][NW][4];
   f4v sf[2];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) acc[1][d] = v4i{0, 0, 0, 0};  // the "previous step" of step 0: zero terms
+  for (int w = 0; w < NW; ++w) {
+    l[w] = g[w] = 0.0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[1][w][d] = v4i{0, 0, 0, 0};  // the "previous step" of step 0: zero terms
+  }
   sf[1] = f4v{0.f, 0.f, 0.f, 0.f};
   stage(0, 0);
   stage(1, 1);
@@ -167,25 +183,29 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
 #pragma unroll
       for (int s = 0; s < KSO; ++s)
 #pragma unroll
-        for (int a = 0; a <= 3 - b; ++a) {
-          const int d = a + b;
-          acc[cur][d] = (b == 0 && s == 0) ? mfma_i8(xa[b & 1][s], wsl[a][s], v4i{0, 0, 0, 0})
-                                           : mfma_i8(xa[b & 1][s], wsl[a][s], acc[cur][d]);
-        }
+        for (int a = 0; a <= 3 - b; ++a)
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const int d = a + b;
+            acc[cur][w][d] = (b == 0 && s == 0) ? mfma_i8(xa[b & 1][s], wsl[w][a][s], v4i{0, 0, 0, 0})
+                                                : mfma_i8(xa[b & 1][s], wsl[w][a][s], acc[cur][w][d]);
+          }
     }
-    row_terms(acc[prv], sf[prv], cz, l, g);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) row_terms(acc[prv][w], sf[prv], cz[w], l[w], g[w]);
     sf[cur] = *(const f4v*)(scl + buf * S::SCB + h * 64 + lk * 16);
-    // one MFMA, then FILL vector instructions, over the 10·KSO MFMAs of the step
+    // one MFMA, then FILL vector instructions, over the 10·KSO·NW MFMAs of the step
     if constexpr (FILL > 0) {
 #pragma unroll
-      for (int i = 0; i < 10 * KSO; ++i) {
+      for (int i = 0; i < 10 * KSO * NW; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, FILL, 0);
       }
     }
     // the row sums are complete here: keeps the row terms in this block (between the MFMAs)
     // instead of sunk past the barrier's wait
-    asm volatile("" ::"v"(l), "v"(g));
+#pragma unroll
+    for (int w = 0; w < NW; ++w) asm volatile("" ::"v"(l[w]), "v"(g[w]));
     step_barrier();
   };
   uint32_t k = 0;
@@ -198,26 +218,31 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   }
   if (k < nsteps) {
     body(k, buf, std::integral_constant<int, 0>{});
-    row_terms(acc[0], sf[0], cz, l, g);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) row_terms(acc[0][w], sf[0], cz[w], l[w], g[w]);
   } else {
-    row_terms(acc[1], sf[1], cz, l, g);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) row_terms(acc[1][w], sf[1], cz[w], l[w], g[w]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero pieces past the end: drained
-  double rs_y = l * rowscale;                       // Σ|ỹ| (exact scaling)
-  double rs_ll = __builtin_fma(g, ln2_alpha, rs_y);
-  rs_ll += __shfl_xor(rs_ll, 16); rs_ll += __shfl_xor(rs_ll, 32);
-  rs_y += __shfl_xor(rs_y, 16);   rs_y += __shfl_xor(rs_y, 32);
-  if (lk == 0) {
-    red[(h * NCP + yi * 16 + lr) * 2 + 0] = rs_ll;
-    red[(h * NCP + yi * 16 + lr) * 2 + 1] = rs_y;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    double rs_y = l[w] * rowscale[w];  // Σ|ỹ| (exact scaling)
+    double rs_ll = __builtin_fma(g[w], ln2_alpha, rs_y);
+    rs_ll += __shfl_xor(rs_ll, 16); rs_ll += __shfl_xor(rs_ll, 32);
+    rs_y += __shfl_xor(rs_y, 16);   rs_y += __shfl_xor(rs_y, 32);
+    if (lk == 0) {
+      red[((w * U + h) * NCP + yi * 16 + lr) * 2 + 0] = rs_ll;
+      red[((w * U + h) * NCP + yi * 16 + lr) * 2 + 1] = rs_y;
+    }
   }
   __syncthreads();
-  double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
-  for (int e = threadIdx.x; e < 2 * NCP; e += 512) {
-    const int c = e / NCP, row = e % NCP;
+  double* out = partials + (size_t)blockIdx.x * NW * 2 * NCP;  // [NW][Σℓ raw | Σ|ỹ|]
+  for (int e = threadIdx.x; e < NW * 2 * NCP; e += 512) {
+    const int w = e / (2 * NCP), c = (e / NCP) % 2, row = e % NCP;
     double v = 0.0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) v += red[(u * NCP + row) * 2 + c];
+    for (int u = 0; u < U; ++u) v += red[((w * U + u) * NCP + row) * 2 + c];
     out[e] = v;
   }
 }
@@ -233,18 +258,19 @@ __global__ void __launch_bounds__(256) k_build_xsf(const double* __restrict__ xs
   }
 }
 
-template <int NB, int FILL>
+template <int NB, int FILL, int NW>
 hipError_t launch_fill(const Screen2Args& a, hipStream_t stream) {
   using S = S2<NB>;
+  constexpr int LDS = S::template lds<NW>();
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB, FILL>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB, FILL, NW>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_screen_oz2<NB, FILL><<<a.nwg, 512, S::LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
-                                                          a.n_blocks, a.partials);
+  k_screen_oz2<NB, FILL, NW><<<a.nwg, 512, LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
+                                                           a.bpw, a.n_blocks, a.partials);
   return hipGetLastError();
 }
 // PICARD_SCREEN2_FILL (measurement knob): vector instructions per MFMA gap, 0 = compiler order.
@@ -257,12 +283,12 @@ int fill_knob() {
   }();
   return v;
 }
-template <int NB>
+template <int NB, int NW>
 hipError_t launch(const Screen2Args& a, hipStream_t stream) {
   switch (fill_knob()) {
-    case 0: return launch_fill<NB, 0>(a, stream);
-    case 2: return launch_fill<NB, 2>(a, stream);
-    default: return launch_fill<NB, 1>(a, stream);
+    case 0: return launch_fill<NB, 0, NW>(a, stream);
+    case 2: return launch_fill<NB, 2, NW>(a, stream);
+    default: return launch_fill<NB, 1, NW>(a, stream);
   }
 }
 
@@ -272,7 +298,8 @@ int screen2_blocks_per_step(int nb) { return 8 / nb; }
 uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }
 
 hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream) {
-  return nb == 8 ? launch<8>(a, stream) : launch<4>(a, stream);
+  if (a.nw == 2) return nb == 8 ? launch<8, 2>(a, stream) : launch<4, 2>(a, stream);
+  return nb == 8 ? launch<8, 1>(a, stream) : launch<4, 1>(a, stream);
 }
 
 hipError_t screen2_build_xsf(const double* xsc, uint64_t n, int e0, float* xsf, hipStream_t stream) {

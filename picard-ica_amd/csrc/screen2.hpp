@@ -20,7 +20,8 @@ struct Screen2Args {
   uint32_t bpw;        // 16-sample blocks per workgroup (a multiple of the blocks per step)
   uint32_t n_blocks;   // 16-sample blocks of the shard
   int nwg;             // workgroups (two per CU)
-  double* partials;    // [nwg][2·16·NB]: [Σℓ raw | Σ|ỹ|] per row
+  double* partials;    // [nwg][nw][2·16·NB]: [Σℓ raw | Σ|ỹ|] per row
+  int nw = 1;          // tries per pass: 2 = the second W in row blocks NB … 2·NB − 1 of the W image
 };
 
 int screen2_blocks_per_step(int nb);   // 16-sample blocks per loop step (NB = 8: 1, NB = 4: 2)
