@@ -45,6 +45,17 @@ for mode in modes:
             ctx.eval_loss_screen(w, mu, d)
         ms, nl = ctx.screen_stats()
         print(f"{mode:5s} N={n} T={t}: screen kernel {ms / max(nl, 1):.3f} ms", flush=True)
+        w2 = np.ascontiguousarray(w[::-1])  # another try of the same shape
+        try:
+            ctx.eval_loss_screen2(w, w2, mu, d)
+            ctx.screen_stats(reset=True)
+            for _ in range(reps):
+                ctx.eval_loss_screen2(w, w2, mu, d)
+            ms, nl = ctx.screen_stats()
+            print(f"{mode:5s} N={n} T={t}: screen pair kernel {ms / max(nl, 1):.3f} ms "
+                  f"({ms / max(nl, 1) / 2:.3f} ms per try)", flush=True)
+        except pa.Unsupported:
+            pass
     ctx.eval(w, mu, d, False, need_y2=False)
     ctx.kernel_breakdown(reset=True)
     for _ in range(reps):
