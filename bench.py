@@ -321,6 +321,7 @@ def main():
     brk = ctx.kernel_breakdown(reset=False)
     int8_timed = ctx.int8_passes - int8_before
     brk["screen"] = ctx.screen_stats(reset=False)
+    screen_tries = ctx.screen_tries()  # a paired pass (two tries) counts 2
 
     if dist is not None:
         import torch
@@ -411,13 +412,19 @@ def main():
             peak, executed = FP64_MFMA_PEAK_TFLOPS, {"fp64_mfma_flops_per_launch": flops}
         if kind == "screen" and i8:
             # a truncated product (a bound, not a pass): priced only against what it executes —
-            # the D <= 3 digit products on the i8 matrix cores
-            tops = executed["i8_ops_per_launch"] / (avg * 1e-3) / 1e12
+            # the D <= 3 digit products on the i8 matrix cores, per TRY
+            # (a paired pass screens two tries: twice the products of a single one)
+            tries = max(screen_tries, nl)
+            per_try_ms = ms / tries
+            executed = dict(executed, i8_ops_per_try=executed.pop("i8_ops_per_launch"))
+            tops = executed["i8_ops_per_try"] / (per_try_ms * 1e-3) / 1e12
             rooflines.append({"bound": "mfma", "achieved": tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
                               "frac": tops / I8_MFMA_PEAK_TOPS, "traffic": pmc.get(short, {}).get("hbm_bytes_per_launch"),
-                              "kernel": label, "avg_kernel_ms": avg, "launches": nl, "ms_per_step": ms / steps,
-                              "executed": executed, "note": "i8 digit products of diagonals D <= 3 against the i8 "
-                              "MFMA issue peak; the fp32 row terms (VALU) are not priced"})
+                              "kernel": label, "avg_kernel_ms": avg, "launches": nl, "tries": tries,
+                              "ms_per_try": per_try_ms, "ms_per_step": ms / steps,
+                              "executed": executed, "note": "i8 digit products of diagonals D <= 3 per screened try "
+                              "against the i8 MFMA issue peak (launches: single and paired passes, avg_kernel_ms "
+                              "mixes both); the fp32 row terms (VALU) are not priced; traffic: a single pass"})
             continue
         rooflines.append({"bound": "mfma", "achieved": tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": tf / FP64_MFMA_PEAK_TFLOPS,
@@ -442,6 +449,7 @@ def main():
                                    "every try exactly: tests/test_gpu_int8.py); screens run inside the timed "
                                    "region and are counted in screen_passes_per_iter") if i8 else "every try exact"},
         "passes_per_iter": passes / steps, "screen_passes_per_iter": brk["screen"][1] / steps,
+        "screened_tries_per_iter": screen_tries / steps,
         "iters_to_tol": iters_to_tol, "converged": converged,
         "total_passes_to_tol": total_passes,
         "whole_fit": ({"samples_per_s_per_iter": T * iters_to_tol / (t_warm + elapsed + t_tol),

@@ -52,9 +52,9 @@ extern "C" {
  * was added (no layout change). 4: PC_ERR_UNSUPPORTED for capability misses of the
  * operator boundary (they no longer abort a rank group). 5: pc_ctx_comm_timing,
  * pc_solver_timing, pc_solver_setup_timing, pc_ctx_alloc_stats, pc_last_teardown,
- * pc_device_mem_info. pc_abi_version() returns the
- * revision the library was built with. */
-#define PC_ABI_VERSION 5
+ * pc_device_mem_info. 6: pc_ctx_eval_loss_screen2 (paired screen), pc_ctx_screen_tries.
+ * pc_abi_version() returns the revision the library was built with. */
+#define PC_ABI_VERSION 6
 
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {
@@ -389,6 +389,8 @@ int pc_ctx_eval_loss_screen2(pc_ctx* ctx, const double* w1, const double* w2, ui
                              char* err, size_t errlen);
 /* line-search screen passes since the last reset: summed HIP-event kernel ms and count */
 void pc_ctx_screen_stats(pc_ctx* ctx, double* kernel_ms, uint64_t* n_launches, int32_t reset);
+/* tries those passes covered since the same reset (a paired pass covers 2) */
+uint64_t pc_ctx_screen_tries(const pc_ctx* ctx);
 /* Exhaustive accuracy of the fp32 instructions the line-search screen evaluates its
  * log-likelihood with (v_exp_f32, v_log_f32), measured on `device` against fp64 libm
  * over every fp32 input of the ranges the screen uses: out[0] max relative error of 2^z

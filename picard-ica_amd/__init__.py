@@ -205,6 +205,7 @@ def _load():
         "pc_ctx_screen_stats": (None, [vp, d, P(u64), i32]),
         "pc_ctx_eval_loss_screen": (C.c_int, [vp, d, u64, d, _Density, d, d, cp, sz]),
         "pc_ctx_eval_loss_screen2": (C.c_int, [vp, d, d, u64, d, _Density, d, d, d, d, cp, sz]),
+        "pc_ctx_screen_tries": (u64, [vp]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -232,7 +233,7 @@ EXPORTED = [
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_ctx_screen_tries", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_solver_timing", "pc_solver_setup_timing", "pc_fit_with_evaluator",
 ]
 
@@ -762,6 +763,11 @@ class DeviceContext:
         _raise(lib.pc_ctx_eval_loss_screen2(self.h, _ptr(w1), _ptr(w2), nc, _ptr(mu_a) if mu_a is not None else None,
                                             density._c(), *[_ptr(o) for o in out], err, len(err)), err)
         return (out[0], out[1]), (out[2], out[3])
+
+    def screen_tries(self) -> int:
+        """pc_ctx_screen_tries: tries the screen passes covered since the last screen_stats reset
+        (a paired pass covers 2)."""
+        return int(lib.pc_ctx_screen_tries(self.h))
 
     def screen_stats(self, reset: bool = False):
         """pc_ctx_screen_stats: (Σ screen-pass kernel ms, screen passes) since the last reset."""

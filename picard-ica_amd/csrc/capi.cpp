@@ -41,6 +41,7 @@ void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int rese
 void device_ctx_set_y_stage(Evaluator* e, int mode);
 uint64_t device_ctx_int8_passes(const Evaluator* e);
 void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset);
+uint64_t device_ctx_screen_tries(const Evaluator* e);
 }  // namespace pcamd
 
 using namespace pcamd;
@@ -520,6 +521,8 @@ int pc_ctx_eval_loss_screen2(pc_ctx* c, const double* w1, const double* w2, uint
 void pc_ctx_screen_stats(pc_ctx* c, double* ms, uint64_t* n, int32_t reset) {
   device_ctx_screen_stats(c->ev.get(), ms, n, reset);
 }
+
+uint64_t pc_ctx_screen_tries(const pc_ctx* c) { return device_ctx_screen_tries(c->ev.get()); }
 
 int pc_device_check_fp32_transcendentals(int32_t device, double out[4]) {
   try {

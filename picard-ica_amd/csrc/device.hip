@@ -3949,6 +3949,7 @@ struct DeviceCtx : Evaluator {
       staged = d2h_enqueue(st_rows, 6 * nc);
     }
     finish_timing(true, 4);
+    ++n_screen_tries;  // the pass covered two tries
     copy_out(tmp.data(), staged, 6 * nc);
     const double kappa1 = 0x1p-22 * 1.0001;
     for (int t = 0; t < 2; ++t) {
@@ -4213,8 +4214,9 @@ struct DeviceCtx : Evaluator {
     if (kind == 1) { sum_loss_ms += a; ++n_loss; }
     if (kind == 2) { sum_fromy_ms += a; ++n_fromy; }
     if (kind == 3) { sum_multi_ms += a; ++n_multi; }
-    if (kind == 4) { sum_screen_ms += a; ++n_screen; }
+    if (kind == 4) { sum_screen_ms += a; ++n_screen; ++n_screen_tries; }
   }
+  uint64_t n_screen_tries = 0;  // tries the screen passes covered (a paired pass: 2)
   double sum_split_ms = 0;
   uint64_t n_split = 0;
 
@@ -4734,8 +4736,9 @@ void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset) {
   auto* d = static_cast<DeviceCtx*>(e);
   *ms = d->sum_screen_ms;
   *n = d->n_screen;
-  if (reset) { d->sum_screen_ms = 0; d->n_screen = 0; }
+  if (reset) { d->sum_screen_ms = 0; d->n_screen = 0; d->n_screen_tries = 0; }
 }
+uint64_t device_ctx_screen_tries(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_screen_tries; }
 void device_check_f32_transc(int device, double* out4) {
   HIP_OK(hipSetDevice(device));
   const int nblk = 2048;
