@@ -196,6 +196,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
     double min_sv = std::numeric_limits<double>::infinity();
     for (size_t i = 0; i < ncomp; ++i) min_sv = std::fmin(min_sv, s[i]);
     if (min_sv < 1e-10) throw singular_matrix();  // whitening.rs:72-79
+    gram_cond_ = (s[0] / min_sv) * (s[0] / min_sv);
     const double sc = std::sqrt(pf);
     K_ = Mat(ncomp, n);
     for (size_t i = 0; i < ncomp; ++i)
@@ -335,14 +336,15 @@ void Solver::init_core() {  // core.rs:175-209
     C_ = Mat::eye(n);
   }
   // whitened covariance for the curvature rejection (orthogonal tanh searches only): used
-  // only when it computes to I within 1e-3, i.e. the whitening is well conditioned
+  // only when it computes to I within 1e-3 and the kept part of the Gram has condition number
+  // below 1e10 (C1's rounding, ≈ 1e-13·cond relative, then stays far inside Cy's 1 % margin)
   if (cfg_.ortho && has_k_ && has_gram_ && cfg_.density.kind == PC_DENSITY_TANH && cfg_.density.alpha > 0.0) {
     C1_ = matmul_nt(matmul(P_, gram_), P_);
     for (double& v : C1_.a) v /= (double)T_;
     double dev = 0.0;
     for (size_t i = 0; i < n; ++i)
       for (size_t j = 0; j < n; ++j) dev = std::fmax(dev, std::fabs(C1_(i, j) - (i == j ? 1.0 : 0.0)));
-    curv_ok_ = dev < 1e-3;
+    curv_ok_ = dev < 1e-3 && gram_cond_ < 1e10;
   }
 }
 
@@ -352,31 +354,38 @@ void Solver::init_core() {  // core.rs:175-209
 // tr(D^k·Cy·D^kᵀ) (A_0 = N_eff) do not depend on α. For the tanh density ℓ′ = tanh(a·y)
 // (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a. The orthogonal loss L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has
 // L′(0) = ⟨g, D⟩ = slope and L″ = u + v with
-//   u(α) = Σ_t Σ_i s_i ℓ″(y_it)(D y_t)_i² / T   ≥ 0 if every s_i = +1, else ≥ −a·A_1;
+//   u(α) = Σ_t Σ_i s_i ℓ″(y_it)(D y_t)_i² / T   ≥ −a·A_1⁻, A_1⁻ = Σ_{i: s_i < 0} (D·Cy·Dᵀ)_ii
+//          (0 when every s_i = +1);
 //   v(α) = Σ_t Σ_i s_i ℓ′(y_it)(D² y_t)_i / T,  v(0) = ⟨g_s, D²⟩ (g_s = s_i·G_ij/T, the
 //          signed gradient before the skew part), |v′| ≤ a·√(A_1·A_2) + a·√(A_0·A_3) = K_3,
-//   |u|, |v| ≤ a·A_1, a·√(A_0·A_2)   (Cauchy–Schwarz over t).
-// Two lower bounds on L(α) − L(0) follow, and the larger is used:
-//   α·slope − α²·M/2, M = a·A_1 + a·√(A_0·A_2);
-//   α·slope + α²·(v(0) − [some s_i < 0]·a·A_1)/2 − α³·K_3/6.
+//          |v| ≤ a·√(A_0·A_2)   (Cauchy–Schwarz over t).
+// So L″(β) ≥ m(β) = max(q − β·K_3, −M) with q = v(0) − a·A_1⁻, M = a·A_1⁻ + a·√(A_0·A_2), and
+//   L(α) − L(0) ≥ α·slope + ∫_0^α (α − β)·m(β) dβ,
+// integrated in closed form on the two pieces of m (the line q − β·K_3 down to β* = (q + M)/K_3,
+// the floor −M after it). Its two extremes are the earlier bounds α·slope − α²·M/2 and
+// α·slope + α²·q/2 − α³·K_3/6, and it is at least the larger of them.
 // When it exceeds the rounding of both exact losses (passes and W(α); far above the kernels'
 // 1e-10 relative sum error), the exact pass at α would reject the try (core.rs:127-140), so it
-// need not run. Cy carries a 2× margin; slope and v(0) are lowered by their rounding bounds.
+// need not run. Cy carries a 1 % margin (C1's rounding is ≈ 1e-13·cond(Gram) relative, and the
+// rejection is off above cond 1e10); slope and v(0) are lowered by their rounding bounds.
 void Solver::set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slope) {
   ls_curv_ = 0.0;
   if (!curv_ok_ || !(slope > 0.0)) return;
   const size_t n = nc_;
-  bool any_neg = false;
-  for (size_t i = 0; i < n; ++i) {
+  for (size_t i = 0; i < n; ++i)
     if (!(signs_[i] == 1.0 || signs_[i] == -1.0)) return;
-    any_neg |= signs_[i] < 0.0;
-  }
   Mat cy = matmul_nt(matmul(W_, C1_), W_);
-  for (double& v : cy.a) v *= 2.0;
+  for (double& v : cy.a) v *= 1.01;
   double a0 = 0.0;
   for (size_t i = 0; i < n; ++i) a0 += cy(i, i);
   const Mat d2 = matmul(d, d), d3 = matmul(d2, d);
-  const double a1 = std::fabs(dot_sum(matmul(d, cy), d));    // tr(D·Cy·Dᵀ) = Σ (D·Cy)∘D
+  const Mat dcy = matmul(d, cy);
+  const double a1 = std::fabs(dot_sum(dcy, d));              // tr(D·Cy·Dᵀ) = Σ (D·Cy)∘D
+  double a1n = 0.0;                                          // its rows with s_i < 0
+  for (size_t i = 0; i < n; ++i)
+    if (signs_[i] < 0.0)
+      for (size_t j = 0; j < n; ++j) a1n += dcy(i, j) * d(i, j);
+  a1n = std::fabs(a1n);
   const double a2 = std::fabs(dot_sum(matmul(d2, cy), d2));  // tr(D²·Cy·D²ᵀ)
   const double a3 = std::fabs(dot_sum(matmul(d3, cy), d3));  // tr(D³·Cy·D³ᵀ)
   double gd = 0.0, gd2 = 0.0, v0 = 0.0;
@@ -387,8 +396,8 @@ void Solver::set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slo
   }
   const double a = cfg_.density.alpha;
   ls_slope_ = slope - 1e-10 * gd;
-  ls_curv_ = a * (a1 + std::sqrt(a0 * a2));
-  ls_q_ = v0 - 1e-10 * gd2 - (any_neg ? a * a1 : 0.0);
+  ls_curv_ = a * (a1n + std::sqrt(a0 * a2));
+  ls_q_ = v0 - 1e-10 * gd2 - a * a1n;
   ls_k3_ = a * (std::sqrt(a1 * a2) + std::sqrt(a0 * a3));
   // |Σ_i ℓ_i| ≤ Σ|y_i| + N·ln2/a ≤ √(N·N_eff) + N·ln2/a per sample
   ls_slack_ = 2.0 * (3e-10 * (std::sqrt((double)n * a0) + (double)n * 0.6931471805599453 / a) + 1e-9);
@@ -398,9 +407,12 @@ void Solver::set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slo
 }
 
 double Solver::curvature_lower_bound(double alpha) const {
-  const double b2 = alpha * ls_slope_ - 0.5 * alpha * alpha * ls_curv_;
-  const double b3 = alpha * ls_slope_ + 0.5 * alpha * alpha * ls_q_ - alpha * alpha * alpha * ls_k3_ / 6.0;
-  return std::fmax(b2, b3);
+  // b: where m(β) meets its floor, within [0, α]
+  double b = ls_k3_ > 0.0 ? (ls_q_ + ls_curv_) / ls_k3_ : (ls_q_ + ls_curv_ >= 0.0 ? alpha : 0.0);
+  b = std::fmin(std::fmax(b, 0.0), alpha);
+  const double r = alpha - b;
+  return alpha * ls_slope_ + ls_q_ * b * (alpha - 0.5 * b) - ls_k3_ * b * b * (0.5 * alpha - b / 3.0) -
+         0.5 * ls_curv_ * r * r;
 }
 
 // Orthogonal line search, host side: W_k = expm(α_k·D)·W (core.rs:118-125) for

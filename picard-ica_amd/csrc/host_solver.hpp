@@ -120,9 +120,11 @@ class Solver {
   bool pairs_ok_ = true;      // false once the evaluator declined a paired screen
   uint64_t screen_pairs_ = 0;  // paired screens (two tries per pass)
   // Curvature rejection of orthogonal tries (Solver::set_curvature): C1 = P·Gram·Pᵀ/T, the
-  // whitened covariance; per search a lower bound on L'(0), a bound on |L''| along
-  // expm(αD)·W and the rounding slack; ls_curv_ = 0 disables
+  // whitened covariance; per search a lower bound on L'(0), the floor −ls_curv_ of L'' along
+  // expm(αD)·W, L''(0)'s lower bound ls_q_ with |L'''|-type slope ls_k3_, and the rounding
+  // slack; ls_curv_ = 0 disables
   bool curv_ok_ = false;
+  double gram_cond_ = 0.0;  // λmax/λmin of the Gram over the kept components (whitening)
   Mat C1_;
   double ls_slope_ = 0.0, ls_curv_ = 0.0, ls_q_ = 0.0, ls_k3_ = 0.0, ls_slack_ = 0.0;
   uint64_t curv_skips_ = 0;

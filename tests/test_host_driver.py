@@ -176,12 +176,14 @@ def test_curvature_rejection_decisions_unchanged(pa, po, dg, capfd, monkeypatch)
 
 @pytest.mark.parametrize("a,mixed", [(1.0, True), (1.0, False), (0.5, True), (2.0, False)])
 def test_curvature_bound_holds(a, mixed):
-    """The bounds behind the curvature rejection (Solver::set_curvature): on whitened data,
-    along W(α) = expm(αD)·W with D skew-symmetric, the tanh loss L(α) = Σ_i s_i mean_t ℓ(y_it)
-    satisfies L(α) − L(0) ≥ max(α·s − α²·M/2, α·s + α²·(v0 − [s_i < 0 somewhere]·a·A1)/2 −
-    α³·K3/6) with A_k = tr(D^k·Cy·D^kᵀ), Cy = mean_t y_t y_tᵀ, M = a·(A1 + √(A0·A2)),
-    K3 = a·(√(A1·A2) + √(A0·A3)), v0 = ⟨g_s, D²⟩ (g_s = s_i·(ψ·Yᵀ)_ij/T), s = ⟨g_s, D⟩
-    (no margins here: the solver doubles Cy)."""
+    """The bound behind the curvature rejection (Solver::set_curvature / curvature_lower_bound):
+    on whitened data, along W(α) = expm(αD)·W with D skew-symmetric, the tanh loss
+    L(α) = Σ_i s_i mean_t ℓ(y_it) satisfies L(α) − L(0) ≥ α·s + ∫_0^α (α − β)·m(β) dβ with
+    m(β) = max(q − β·K3, −M), A_k = tr(D^k·Cy·D^kᵀ), Cy = mean_t y_t y_tᵀ, A1⁻ = the rows of A1
+    with s_i < 0, q = v0 − a·A1⁻, M = a·(A1⁻ + √(A0·A2)), K3 = a·(√(A1·A2) + √(A0·A3)),
+    v0 = ⟨g_s, D²⟩ (g_s = s_i·(ψ·Yᵀ)_ij/T), s = ⟨g_s, D⟩ (no margins here: the solver takes
+    1.01·Cy). The bound is at least the round-2 pair max(α·s − α²·a·(A1 + √(A0·A2))/2,
+    α·s + α²·q/2 − α³·K3/6)."""
     from scipy.linalg import expm
     rng = np.random.default_rng(5)
     n, t = 8, 4000
@@ -208,11 +210,17 @@ def test_curvature_bound_holds(a, mixed):
         slope = float(np.sum(gs * d))
         d2 = d @ d
         a0, a1, a2, a3 = float(np.trace(cy)), tr(d), tr(d2), tr(d2 @ d)
-        m = a * (a1 + np.sqrt(a0 * a2))
-        q = float(np.sum(gs * d2)) - (a * a1 if np.any(s < 0) else 0.0)
+        a1n = float(np.sum(((d @ cy) * d)[s < 0]))
+        m_old = a * (a1 + np.sqrt(a0 * a2))
+        m = a * (a1n + np.sqrt(a0 * a2))
+        q = float(np.sum(gs * d2)) - a * a1n
         k3 = a * (np.sqrt(a1 * a2) + np.sqrt(a0 * a3))
         for alpha in 2.0 ** -np.arange(0, 10):
             lhs = loss(expm(alpha * d) @ w) - loss(w)
-            b2 = alpha * slope - alpha * alpha * m / 2
+            b = min(max((q + m) / k3, 0.0), alpha)
+            bound = (alpha * slope + q * b * (alpha - b / 2) - k3 * b * b * (alpha / 2 - b / 3)
+                     - m * (alpha - b) ** 2 / 2)
+            b2 = alpha * slope - alpha * alpha * m_old / 2
             b3 = alpha * slope + alpha * alpha * q / 2 - alpha ** 3 * k3 / 6
-            assert lhs >= max(b2, b3) - 1e-12, (alpha, lhs, b2, b3)
+            assert bound >= max(b2, b3) - 1e-15 * (1 + abs(bound)), (alpha, bound, b2, b3)
+            assert lhs >= bound - 1e-12, (alpha, lhs, bound)
