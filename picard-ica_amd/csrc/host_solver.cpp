@@ -654,7 +654,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     // Curvature rejection (set_curvature): once the evaluator has shown that it screens (so
     // the exact-every-try modes keep every pass), a try the bound already rejects needs no pass
     if (ortho && ls_curv_ > 0.0 && screen_seen_ && curvature_lower_bound(alpha) > ls_slack_) {
-      if (k == 0 && !first_loss_only && !full_first) first_n_[first_full_ ? 1 : 0] += 1.0;
+      if (k == 0 && !first_loss_only && !full_first) first_n_[first_cell_] += 1.0;
       ++curv_skips_;
       r.screened_out = true;  // no exact statistics for this W
       if (trace_)
@@ -666,9 +666,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     // Orthogonal searches screen their tries when the evaluator has a screen. Try 1 of a
     // descent direction (⟨g, D⟩ < 0) is accepted with some probability p: screening it
     // costs t_s + p·t_f against t_f for a full pass, so it is screened only while the
-    // running estimate of p is below 1 − t_s/t_f (measured running means). p is estimated
-    // per state of the previous search (accepted at try 1 or not: on C3 the first tries
-    // alternate, 0.6 vs 1.0 acceptance), Laplace-smoothed over this fit's first tries.
+    // running estimate of p is below 1 − t_s/t_f. p is estimated per cell (step(): whether
+    // Picard's quadratic model along D predicts a decrease at α = 1, and whether the previous
+    // search was accepted at try 1) over this fit's first tries.
     // t_s/t_f: screen_cost_ratio (rank-independent; see below).
     // The gradient fallback (full_first) is accepted at try 1 almost always: full pass.
     // Schedule only: no decision changes.
@@ -680,9 +680,11 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       } else if (first_policy) {
         // t_s/t_f is a model of the shape, not the measured means: with one RCCL
         // communicator every rank must take the same branch (the screen and the full
-        // pass issue different all-reduces), and p_acc is built from decisions alone
-        const int st = first_full_ ? 1 : 0;
-        const double p_acc = (first_acc_[st] + 1.0) / (first_n_[st] + 2.0);
+        // pass issue different all-reduces), and p_acc is built from decisions alone.
+        // p per policy cell, Beta-prior mean: Beta(9, 1) where the model predicts a decrease
+        // (a full pass from the start; two early failures bring screening back), else Beta(1, 1)
+        const int c = first_cell_;
+        const double p_acc = c >= 2 ? (first_acc_[c] + 9.0) / (first_n_[c] + 10.0) : (first_acc_[c] + 1.0) / (first_n_[c] + 2.0);
         screen = p_acc < 1.0 - screen_cost_ratio(n, T_);
       }
     }
@@ -766,7 +768,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         }
       }
       if (rejected) {
-        if (first_policy) first_n_[first_full_ ? 1 : 0] += 1.0;
+        if (first_policy) first_n_[first_cell_] += 1.0;
         ++screen_rejects_;
         r.screened_out = true;  // no exact statistics for this W
         alpha /= 2.0;
@@ -792,8 +794,8 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     r.loss = loss_of(r.stats, r.w, signs_, &singular);
     const bool accepted = r.loss < current_loss_;
     if (first_policy) {
-      first_n_[first_full_ ? 1 : 0] += 1.0;
-      if (accepted) first_acc_[first_full_ ? 1 : 0] += 1.0;
+      first_n_[first_cell_] += 1.0;
+      if (accepted) first_acc_[first_cell_] += 1.0;
     }
     if (accepted) {
       r.success = true;
@@ -902,6 +904,21 @@ bool Solver::step() {
   // the wasted G stage. An accepted try is completed either way.
   const double slope = dot_sum(g, direction);
   set_curvature(g, gs, direction, slope);
+  // First-try policy cell (schedule only): Picard's quadratic model along D, L(α) − L(0) ≈
+  // α·slope + α²·qh/2 with qh = Σ h_ij·D_ij² (the Hessian approximation that preconditions D),
+  // predicts a decrease at α = 1 when slope + qh/2 < 0 — exactly −slope/2 for the plain Newton
+  // step. On C3 every first try with that prediction was accepted, and 25 of 27 without it that
+  // followed an accepted search failed (profiles/r04_j). Computed from rank-identical data.
+  {
+    double qh = 0.0;
+    if (ortho)
+      for (size_t e = 0; e < n * n; ++e) qh += h.a[e] * direction.a[e] * direction.a[e];
+    const bool model_decrease = ortho && slope < 0.0 && slope + 0.5 * qh < 0.0;
+    first_cell_ = (model_decrease ? 2 : 0) + (first_full_ ? 1 : 0);
+    if (trace_ && ortho)
+      std::fprintf(stderr, "[picard-pred] iter %zu slope %.6e qh %.6e model %.3e first_full %d cell %d\n", iter_ + 1, slope,
+                   qh, slope + 0.5 * qh, first_full_ ? 1 : 0, first_cell_);
+  }
   LsResult res = line_search(direction, cfg_.ls_tries, !first_full_, ortho && slope >= 0.0);
   const size_t first_tries = res.tries;
   const bool first_ok = res.success;

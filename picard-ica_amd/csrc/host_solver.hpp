@@ -131,7 +131,10 @@ class Solver {
   void set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slope);
   double curvature_lower_bound(double alpha) const;
   // first-try policy: outcomes of descent-direction first tries
-  double first_n_[2] = {0.0, 0.0}, first_acc_[2] = {0.0, 0.0};  // by state: previous search accepted at try 1?
+  // by cell: 2·(Picard's quadratic model predicts a decrease at α = 1) + (previous search accepted
+  // at try 1); first_cell_ is this iteration's (set in step)
+  double first_n_[4] = {0.0, 0.0, 0.0, 0.0}, first_acc_[4] = {0.0, 0.0, 0.0, 0.0};
+  int first_cell_ = 0;
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are
