@@ -907,8 +907,9 @@ bool Solver::step() {
   // First-try policy cell (schedule only): Picard's quadratic model along D, L(α) − L(0) ≈
   // α·slope + α²·qh/2 with qh = Σ h_ij·D_ij² (the Hessian approximation that preconditions D),
   // predicts a decrease at α = 1 when slope + qh/2 < 0 — exactly −slope/2 for the plain Newton
-  // step. On C3 every first try with that prediction was accepted, and 25 of 27 without it that
-  // followed an accepted search failed (profiles/r04_j). Computed from rank-identical data.
+  // step. On the traced C3 and proxy fits every first try with that prediction was accepted (34),
+  // and 17 of 19 without it that followed an accepted search failed (profiles/r04_j). Computed
+  // from rank-identical data.
   {
     double qh = 0.0;
     if (ortho)
