@@ -674,6 +674,17 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     // Schedule only: no decision changes.
     bool screen = ortho && !keep_y_ && screen_ok_;
     const bool first_policy = k == 0 && !first_loss_only && !full_first;
+    // A later try of a descent search (its first try failed) where Picard's quadratic model
+    // still predicts a decrease, α·slope + α²·qh/2 < 0: the same estimate as try 1's cells
+    // (Beta(9, 1) prior, own counts). On the traced proxy fit it named the accepted try of
+    // every such search it reached (profiles/r04_k). Schedule only.
+    const bool later_policy = k > 0 && !first_loss_only && !full_first && pred_slope_ < 0.0 && pred_qh_ > 0.0 &&
+                              pred_slope_ + 0.5 * alpha * pred_qh_ < 0.0;
+    bool later_full = false;
+    if (screen && later_policy && (later_acc_ + 9.0) / (later_n_ + 10.0) >= 1.0 - screen_cost_ratio(n, T_)) {
+      screen = false;
+      later_full = true;
+    }
     if (screen && k == 0) {
       if (full_first) {
         screen = false;
@@ -688,7 +699,8 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         screen = p_acc < 1.0 - screen_cost_ratio(n, T_);
       }
     }
-    if (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_)) {
+    if (later_full || (!screen && k == 0 && !first_loss_only && (first_full_ || !split_first_))) {
+      if (later_full && trace_) std::fprintf(stderr, "[picard-model] try %zu alpha %.3e full pass\n", k + 1, alpha);
       evaluate(r.w, &r.stats);
       r.partial = false;
     } else if (screen) {
@@ -769,6 +781,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       }
       if (rejected) {
         if (first_policy) first_n_[first_cell_] += 1.0;
+        if (later_policy) later_n_ += 1.0;
         ++screen_rejects_;
         r.screened_out = true;  // no exact statistics for this W
         alpha /= 2.0;
@@ -796,6 +809,10 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     if (first_policy) {
       first_n_[first_cell_] += 1.0;
       if (accepted) first_acc_[first_cell_] += 1.0;
+    }
+    if (later_policy) {
+      later_n_ += 1.0;
+      if (accepted) later_acc_ += 1.0;
     }
     if (accepted) {
       r.success = true;
@@ -916,6 +933,8 @@ bool Solver::step() {
       for (size_t e = 0; e < n * n; ++e) qh += h.a[e] * direction.a[e] * direction.a[e];
     const bool model_decrease = ortho && slope < 0.0 && slope + 0.5 * qh < 0.0;
     first_cell_ = (model_decrease ? 2 : 0) + (first_full_ ? 1 : 0);
+    pred_slope_ = ortho ? slope : 0.0;
+    pred_qh_ = ortho ? qh : 0.0;
     if (trace_ && ortho)
       std::fprintf(stderr, "[picard-pred] iter %zu slope %.6e qh %.6e model %.3e first_full %d cell %d\n", iter_ + 1, slope,
                    qh, slope + 0.5 * qh, first_full_ ? 1 : 0, first_cell_);

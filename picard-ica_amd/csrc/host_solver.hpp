@@ -135,6 +135,8 @@ class Solver {
   // at try 1); first_cell_ is this iteration's (set in step)
   double first_n_[4] = {0.0, 0.0, 0.0, 0.0}, first_acc_[4] = {0.0, 0.0, 0.0, 0.0};
   int first_cell_ = 0;
+  // the model along this iteration's D (slope, qh) and the later-try cell's counts
+  double pred_slope_ = 0.0, pred_qh_ = 0.0, later_n_ = 0.0, later_acc_ = 0.0;
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are

@@ -262,12 +262,14 @@ def test_screen_unavailable_shapes(pa, rng):
         ctx.eval_loss_screen(np.eye(100), x.mean(axis=1), pa.DensityType.tanh())
 
 
-@pytest.mark.parametrize("n,seed", [(128, 42), (96, 7), (64, 42), (48, 3)])
-def test_screened_fit_bit_identical(pa, n, seed, capfd, monkeypatch):
+@pytest.mark.parametrize("n,seed,model", [(128, 42, True), (96, 7, False), (64, 42, True), (48, 3, True)])
+def test_screened_fit_bit_identical(pa, n, seed, model, capfd, monkeypatch):
     """A Picard-O fit with the line-search screen (default) and without it (int8-exact):
     identical iterations and bit-identical unmixing — the screen rejects only tries the
     exact pass would reject. The bench mixture (benches/benchmarks.rs) has line searches
-    that fail all 10 tries, so the screen does reject some (counted in the trace)."""
+    that fail all 10 tries, so the screen does reject some (counted in the trace). `model`:
+    the fit also runs later tries as full passes by the quadratic-model policy ("[picard-model]",
+    Solver::line_search), whose schedule must not change a bit either."""
     monkeypatch.setenv("PICARD_TRACE", "1")
     res = {}
     for mode in ("auto", "int8-exact"):
@@ -286,6 +288,7 @@ def test_screened_fit_bit_identical(pa, n, seed, capfd, monkeypatch):
     assert np.array_equal(r.unmixing, r0.unmixing)
     rejected = [int(line.split("rejected ")[1].split()[0]) for line in err.splitlines() if "rejected " in line]
     assert rejected and max(rejected) > 0
+    assert "[picard-model]" in err or not model
 
 
 @pytest.mark.parametrize("t", [16 * 512 * 7 + 5, 1_000_003])
