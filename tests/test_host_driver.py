@@ -224,3 +224,34 @@ def test_curvature_bound_holds(a, mixed):
             b3 = alpha * slope + alpha * alpha * q / 2 - alpha ** 3 * k3 / 6
             assert bound >= max(b2, b3) - 1e-15 * (1 + abs(bound)), (alpha, bound, b2, b3)
             assert lhs >= bound - 1e-12, (alpha, lhs, bound)
+
+
+@pytest.mark.parametrize("n,t,seed", [(16, 20000, 42), (24, 20000, 42)])
+def test_model_schedule_decisions_unchanged(pa, po, dg, n, t, seed, capfd, monkeypatch):
+    """The quadratic-model schedule (Solver::step's first-try cells, line_search's later-try
+    full passes, "[picard-model]") changes no decision: with a screen the fit runs some later
+    tries as full passes straight away, and stays bit-identical to the every-try-exact fit."""
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    x, _ = dg.generate_data(n, t, seed)[:2]
+
+    def ev(w, mu, d, need_h):
+        return po.pass_stats(w, mu, x, density_of(po, d), need_h)
+
+    def screen(w, mu, d):
+        ll = po.pass_stats(w, mu, x, density_of(po, d), False)["ll"]
+        return ll, 1e-9 * np.abs(ll) + 1e-12
+
+    def fit(with_screen):
+        kw = dict(eval_loss_screen=screen) if with_screen else {}
+        return pa.fit_with_host_evaluator(
+            x.shape[0], x.shape[1], pa.PicardConfig(random_state=42, max_iter=60),
+            rowsum=lambda: x.sum(axis=1), gram=lambda mu: (x - mu[:, None]) @ (x - mu[:, None]).T,
+            eval=ev, sources=lambda w, mu: w @ (x - mu[:, None]), **kw)
+
+    r0 = fit(False)
+    capfd.readouterr()
+    r1 = fit(True)
+    err = capfd.readouterr().err
+    assert "[picard-model]" in err and "[picard-pred]" in err
+    assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
+    assert np.array_equal(r1.unmixing, r0.unmixing)
