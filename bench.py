@@ -331,6 +331,7 @@ def main():
 
     iters_to_tol, converged, total_passes = None, None, None
     t_tol = None
+    amari_c3 = None
     transform = None
     if args.to_tol:
         t1 = time.perf_counter()
@@ -344,6 +345,8 @@ def main():
         # (int8-digit store k_ystore_oz when the fit left the digit image resident: reads the
         # 7-byte digits + 2^e_t per sample, writes 8 B per element; else the fp64 k_ystore)
         wf = res.full_unmixing()
+        # Amari distance of the fitted unmixing against the generated mixing (N×N, host)
+        amari_c3 = float(pa.utils.amari_distance(wf, a_mix))
         n8 = ctx.int8_passes
         tr_ms = [ctx.sources_device(wf, res.mean)[2] for _ in range(3)]
         tr_i8 = ctx.int8_passes > n8
@@ -474,6 +477,13 @@ def main():
         out["timings_s"]["close"] = time.perf_counter() - t_close
         out["timings_s"]["close_teardown"] = {k: round(v, 3) for k, v in pa.last_teardown().items()}
         out["other_configs"] = {k: run_config(pa, k, args.seed, cpu=bool(args.cpu_baseline)) for k in OTHER_CONFIGS}
+    # the metric's second half and the fit's evidence LAST, so a reader of only the tail of the
+    # line (the driver keeps the end of stdout) sees them
+    tail_keys = ("passes_per_iter", "screen_passes_per_iter", "whole_fit", "iters_to_tol", "converged")
+    for k in tail_keys:
+        out[k] = out.pop(k)
+    out["amari_vs_true_mixing"] = amari_c3
+    out["window"] = {"warmup": args.warmup, "steps": steps_run, "ms_per_step": ms_per_step, "value": value}
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -2653,11 +2653,16 @@ struct DeviceCtx : Evaluator {
       if (sl->p) (void)hipHostFree(sl->p);
       if (sl->ev) (void)hipEventDestroy(sl->ev);
     }
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
     // the release as a whole: hipDeviceSynchronize charges any deferred work of the frees to
-    // this teardown instead of to the next context's first allocation
+    // this teardown instead of to the next context's first allocation —
+    // only when no other context of this process lives on the device, so closing one rank of an
+    // in-process group (or an error path) never waits for another context's work
     const auto ts = std::chrono::steady_clock::now();
-    (void)hipDeviceSynchronize();
+    if (ctxs_on_device(device) == 0) (void)hipDeviceSynchronize();
     const double sync_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     std::lock_guard<std::mutex> lk(g_teardown_mu);
     g_teardown[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td0).count();
@@ -3792,7 +3797,8 @@ struct DeviceCtx : Evaluator {
   int screen_agreed_ = 0, ybuf_agreed_ = 0;
   uint64_t n_agree_ = 0;
   bool pin_test_ = false;  // PICARD_TEST_PIN_DIGITS=1: pin the image without a group (tests)
-  bool xsl_pinned() const { return (coll_ && screen_agreed_ == 1) || pin_test_; }
+  // (either agreement pins it: a paired screen may be the first screen of a fit)
+  bool xsl_pinned() const { return (coll_ && (screen_agreed_ == 1 || screen_pair_agreed_ == 1)) || pin_test_; }
   bool agree_once(int& state, bool local, const char* what) {
     if (state == 0) {
       ++n_agree_;
@@ -4460,7 +4466,7 @@ struct DeviceCtx : Evaluator {
     // [A: npos·np][V: n·n][granules: 2·3·G {value, seq} pairs][θ log: cap + 1][sweep counts]
     const int theta_cap = (int)std::min<size_t>(max_iter / 10, 1u << 16);
     const size_t off_v = npos * np, off_g = off_v + n * n, off_th = off_g + 2 * G * 3 * 2,
-                 off_sw = off_th + (size_t)theta_cap + 1, total = off_sw + 1;
+                 off_sw = off_th + (size_t)theta_cap + 1, total = off_sw + 2;
     double* base = ensure(d_jade, cap_jade, total);
     double *d_a = base, *d_v = base + off_v, *d_g = base + off_g, *d_th = base + off_th;
     int* d_sw = (int*)(base + off_sw);
@@ -4470,7 +4476,7 @@ struct DeviceCtx : Evaluator {
     if (const char* e = std::getenv("PICARD_JADE_BAR_BASE")) seq0 = std::strtoull(e, nullptr, 0);
     long long max_pairs = (long long)std::min<size_t>(jade_max_pairs(), (size_t)LLONG_MAX);
     HIP_OK(hipMemsetAsync(d_g, 0, 2 * G * 3 * 2 * sizeof(double), stream));  // tags 0 ≠ any seq ≥ seq0 + 1
-    HIP_OK(hipMemsetAsync(d_sw, 0, 2 * sizeof(int), stream));
+    HIP_OK(hipMemsetAsync(d_sw, 0, 4 * sizeof(int), stream));  // sweeps, converged, stalled
     if (A) {
       HIP_OK(hipMemcpyAsync(d_a, A, npos * np * sizeof(double), hipMemcpyHostToDevice, stream));
     } else {
@@ -4485,7 +4491,9 @@ struct DeviceCtx : Evaluator {
     // device launches it plainly; contexts that share the device (an in-process rank group, or
     // several contexts of one process) use the cooperative launch, whose admission guarantees
     // co-residency against each other's sweeps. (A rocprofv3-traced process that ran a
-    // cooperative launch crashed in HIP's exit handler: DESIGN.md §6.) A refused launch is not
+    // cooperative launch crashed in HIP's exit handler: DESIGN.md §6.) A plain launch that is
+    // not co-resident after all (another process holding CUs) cannot hang: each workgroup's
+    // wait is bounded (JS_POLL_CAP) and a stalled grid reports it. A refused launch is not
     // an error: the host sweeps run instead (PICARD_TEST_JADE_REFUSE=1 refuses every launch,
     // a test hook).
     const bool coop_launch = (coll_ && std::strcmp(coll_->kind(), "local") == 0) || ctxs_on_device(device) > 1;
@@ -4506,10 +4514,13 @@ struct DeviceCtx : Evaluator {
       sync();  // the queued copies into the buffer are done before it is reused
       return false;
     }
-    int sw[2] = {0, 0};
+    int sw[3] = {0, 0, 0};
     HIP_OK(hipMemcpyAsync(v_out, d_v, n * n * sizeof(double), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipMemcpyAsync(sw, d_sw, 2 * sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(sw, d_sw, 3 * sizeof(int), hipMemcpyDeviceToHost, stream));
     sync();
+    // a workgroup gave up waiting for the others' granules (the grid was not co-resident:
+    // JS_POLL_CAP): V is partial, the host sweeps run instead
+    if (sw[2] != 0) return false;
     log->sweeps = (size_t)sw[0];
     log->converged = sw[1] != 0;
     log->theta10.assign(std::min<size_t>(log->sweeps / 10, (size_t)theta_cap), 0.0);

@@ -354,8 +354,8 @@ void Solver::init_core() {  // core.rs:175-209
 // tr(D^k·Cy·D^kᵀ) (A_0 = N_eff) do not depend on α. For the tanh density ℓ′ = tanh(a·y)
 // (|ℓ′| ≤ a|y|) and 0 ≤ ℓ″ ≤ a. The orthogonal loss L(α) = Σ_i s_i Σ_t ℓ(y_it)/T has
 // L′(0) = ⟨g, D⟩ = slope and L″ = u + v with
-//   u(α) = Σ_t Σ_i s_i ℓ″(y_it)(D y_t)_i² / T   ≥ −a·A_1⁻, A_1⁻ = Σ_{i: s_i < 0} (D·Cy·Dᵀ)_ii
-//          (0 when every s_i = +1);
+//   u(α) = Σ_t Σ_i s_i ℓ″(y_it)(D y_t)_i² / T   ≥ −a·A_1⁻, A_1⁻ = min(A_1, λmax(Cy)·Σ_{i: s_i < 0} (D·Dᵀ)_ii)
+//          (0 when every s_i = +1; both terms bound the negative rows at every α, below);
 //   v(α) = Σ_t Σ_i s_i ℓ′(y_it)(D² y_t)_i / T,  v(0) = ⟨g_s, D²⟩ (g_s = s_i·G_ij/T, the
 //          signed gradient before the skew part), |v′| ≤ a·√(A_1·A_2) + a·√(A_0·A_3) = K_3,
 //          |v| ≤ a·√(A_0·A_2)   (Cauchy–Schwarz over t).
@@ -381,11 +381,22 @@ void Solver::set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slo
   const Mat d2 = matmul(d, d), d3 = matmul(d2, d);
   const Mat dcy = matmul(d, cy);
   const double a1 = std::fabs(dot_sum(dcy, d));              // tr(D·Cy·Dᵀ) = Σ (D·Cy)∘D
-  double a1n = 0.0;                                          // its rows with s_i < 0
+  // A1⁻ bounds Σ_{s_i<0} (E·D·Cy·Dᵀ·Eᵀ)_ii at EVERY α (E = expm(αD)): a partial diagonal sum
+  // is not rotation-invariant, but D·Cy·Dᵀ ≤ λmax(Cy)·D·Dᵀ and E·D·Dᵀ·Eᵀ = D·Dᵀ (E commutes
+  // with D and is orthogonal), so A1⁻ = λ·Σ_{s_i<0} (D·Dᵀ)_ii with λ ≥ λmax(Cy) from
+  // Gershgorin, capped by the invariant full trace A1 (exact for any Cy, not only
+  // an isotropic one)
+  double lam = 0.0;
+  for (size_t i = 0; i < n; ++i) {
+    double r = 0.0;
+    for (size_t j = 0; j < n; ++j) r += std::fabs(cy(i, j));
+    lam = std::fmax(lam, r);
+  }
+  double ddn = 0.0;
   for (size_t i = 0; i < n; ++i)
     if (signs_[i] < 0.0)
-      for (size_t j = 0; j < n; ++j) a1n += dcy(i, j) * d(i, j);
-  a1n = std::fabs(a1n);
+      for (size_t j = 0; j < n; ++j) ddn += d(i, j) * d(i, j);
+  const double a1n = std::fmin(a1, lam * ddn);
   const double a2 = std::fabs(dot_sum(matmul(d2, cy), d2));  // tr(D²·Cy·D²ᵀ)
   const double a3 = std::fabs(dot_sum(matmul(d3, cy), d3));  // tr(D³·Cy·D³ᵀ)
   double gd = 0.0, gd2 = 0.0, v0 = 0.0;

@@ -174,8 +174,9 @@ def test_curvature_rejection_decisions_unchanged(pa, po, dg, capfd, monkeypatch)
     assert np.array_equal(r1.unmixing, r0.unmixing)
 
 
-@pytest.mark.parametrize("a,mixed", [(1.0, True), (1.0, False), (0.5, True), (2.0, False)])
-def test_curvature_bound_holds(a, mixed):
+@pytest.mark.parametrize("a,mixed,aniso", [(1.0, True, False), (1.0, False, False), (0.5, True, False),
+                                           (2.0, False, False), (1.0, True, True), (2.0, True, True)])
+def test_curvature_bound_holds(a, mixed, aniso):
     """The bound behind the curvature rejection (Solver::set_curvature / curvature_lower_bound):
     on whitened data, along W(α) = expm(αD)·W with D skew-symmetric, the tanh loss
     L(α) = Σ_i s_i mean_t ℓ(y_it) satisfies L(α) − L(0) ≥ α·s + ∫_0^α (α − β)·m(β) dβ with
@@ -183,7 +184,9 @@ def test_curvature_bound_holds(a, mixed):
     with s_i < 0, q = v0 − a·A1⁻, M = a·(A1⁻ + √(A0·A2)), K3 = a·(√(A1·A2) + √(A0·A3)),
     v0 = ⟨g_s, D²⟩ (g_s = s_i·(ψ·Yᵀ)_ij/T), s = ⟨g_s, D⟩ (no margins here: the solver takes
     1.01·Cy). The bound is at least the round-2 pair max(α·s − α²·a·(A1 + √(A0·A2))/2,
-    α·s + α²·q/2 − α³·K3/6)."""
+    α·s + α²·q/2 − α³·K3/6). A1⁻ = min(A1, λ·Σ_{s_i<0}(D·Dᵀ)_ii), λ = the Gershgorin bound on
+    λmax(Cy): it bounds the negative rows at every α, so the bound holds for an anisotropic Cy
+    too (aniso: rows scaled up to 4x after whitening)."""
     from scipy.linalg import expm
     rng = np.random.default_rng(5)
     n, t = 8, 4000
@@ -191,8 +194,13 @@ def test_curvature_bound_holds(a, mixed):
     x -= x.mean(axis=1, keepdims=True)
     ev, u = np.linalg.eigh(x @ x.T / t)
     x = (u / np.sqrt(ev)).T @ x  # whitened: covariance I
+    if aniso:  # far from isotropic, with a rotation so Cy is not diagonal
+        q0 = np.linalg.qr(rng.normal(size=(n, n)))[0]
+        x = q0 @ (np.geomspace(0.25, 4.0, n)[:, None] * x)
     w = np.linalg.qr(rng.normal(size=(n, n)))[0]
     s = np.sign(rng.normal(size=n)) if mixed else np.ones(n)
+    if aniso:
+        s[: n // 2] = -1.0  # several negative rows
 
     def ell(y):  # density.rs Tanh log_lik: |y| + log1p(exp(-2a|y|))/a
         return np.abs(y) + np.log1p(np.exp(-2 * a * np.abs(y))) / a
@@ -210,7 +218,8 @@ def test_curvature_bound_holds(a, mixed):
         slope = float(np.sum(gs * d))
         d2 = d @ d
         a0, a1, a2, a3 = float(np.trace(cy)), tr(d), tr(d2), tr(d2 @ d)
-        a1n = float(np.sum(((d @ cy) * d)[s < 0]))
+        lam = float(np.max(np.sum(np.abs(cy), axis=1)))
+        a1n = min(a1, lam * float(np.sum((d * d)[s < 0])))
         m_old = a * (a1 + np.sqrt(a0 * a2))
         m = a * (a1n + np.sqrt(a0 * a2))
         q = float(np.sum(gs * d2)) - a * a1n
