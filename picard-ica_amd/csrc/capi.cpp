@@ -39,6 +39,8 @@ void device_mem_info(int device, uint64_t* free_b, uint64_t* total_b);
 void device_check_f32_transc(int device, double* out4);
 void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int reset);
 void device_ctx_set_y_stage(Evaluator* e, int mode);
+void device_ctx_set_g_stage(Evaluator* e, int mode);
+uint64_t device_ctx_g8_passes(const Evaluator* e);
 uint64_t device_ctx_int8_passes(const Evaluator* e);
 void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset);
 uint64_t device_ctx_screen_tries(const Evaluator* e);
@@ -500,6 +502,14 @@ int pc_ctx_set_y_stage(pc_ctx* c, int32_t mode) {
 }
 
 uint64_t pc_ctx_int8_passes(const pc_ctx* c) { return device_ctx_int8_passes(c->ev.get()); }
+
+int pc_ctx_set_g_stage(pc_ctx* c, int32_t mode) {
+  if (mode != PC_GSTAGE_AUTO && mode != PC_GSTAGE_F64) return PC_ERR_INVALID_CONFIG;
+  device_ctx_set_g_stage(c->ev.get(), mode);
+  return PC_OK;
+}
+
+uint64_t pc_ctx_g8_passes(const pc_ctx* c) { return device_ctx_g8_passes(c->ev.get()); }
 
 int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density density,
                             double* ll_out, double* bound_out, char* err, size_t errlen) {

@@ -877,6 +877,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 // formulas as k_eval_fused<8> / k_eval_loss<8> / k_eval_fromy<8>: identical sums.
 // ---------------------------------------------------------------------------
 #include "fused_ws.inc"
+#include "fused_g8.inc"  // the same pass with G = ψ·Yᵀ on int8 digits too
 
 // ---------------------------------------------------------------------------
 // Split evaluation for line-search tries (bit-identical sums to k_eval_fused):
@@ -2993,6 +2994,32 @@ struct DeviceCtx : Evaluator {
     // the digit-stage forms of the warp-specialised kernels never read the fp64 W: its copy is
     // left out of the call's timeline
     if (!((ws && oz) || (!ws && ws4 && oz4))) flush_wp();
+    // … and with G = ψ·Yᵀ on the i8 matrix cores too (fused_g8.inc): bounded ψ (tanh, exp), the
+    // row scales of the W image built for this image's exponent range (upload_wsl)
+    constexpr bool G8D = D == DENS_TANH || D == DENS_EXP;
+    const bool g8 = G8D && oz && g_stage_ == 0 && g8_scales_ok_ && g8_emax_ == xsc_emax_ && nf <= 128;
+    if (g8) {
+      if constexpr (G8D) {
+        double psc = 0x1p46;  // tanh: |ψ| ≤ 1
+        if (D == DENS_EXP) {  // |ψ| = |y|·e^{−αy²/2} ≤ 1/√(α·e) < 2^Fψ
+          const double bound = 1.0 / std::sqrt(alpha * 2.718281828459045) * (1.0 + 1e-12);
+          psc = std::ldexp(1.0, 46 - (std::ilogb(bound) + 1));
+        }
+        auto kg8 = k_eval_fused_g8<D, Q>;
+        lds_attr((const void*)kg8, G8_LDS);
+        HIP_OK(hipEventRecord(ev[1], stream));
+        kg8<<<nwg, WS_THREADS, G8_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc, g8_dbg_);
+        HIP_OK(hipGetLastError());
+        ++n_int8_passes_;
+        ++n_g8_passes_;
+        HIP_OK(hipEventRecord(ev[2], stream));
+        const size_t total = EvalStats::size(nc, H);
+        k_reduce<<<(total + RED_OUT - 1) / RED_OUT, 256, 0, stream>>>(part, nwg, pstride, S::NCP, (int)nc, H, st, D,
+                                                                      alpha, (double)n_local_);
+        HIP_OK(hipGetLastError());
+        return;
+      }
+    }
     auto kws = oz ? k_eval_fused_ws<D, Q, true> : k_eval_fused_ws<D, Q, false>;
     auto kfu = oz4 ? k_eval_fused<NB, H, D, Q, OZ4> : k_eval_fused<NB, H, D, Q, false>;
     auto kw4 = oz4 ? k_eval_fused_ws4<D, Q, OZ4> : k_eval_fused_ws4<D, Q, false>;
@@ -3555,6 +3582,16 @@ struct DeviceCtx : Evaluator {
   double* d_wsc = nullptr;
   int y_stage_ = 0;
   uint64_t n_int8_passes_ = 0;
+  // G = ψ·Yᵀ on int8 digits (fused_g8.inc): g_stage_ 0 = where the shape allows, 1 = the fp64 G
+  // stage (the default until the digit stage is the faster one; PICARD_G8=1 or
+  // pc_ctx_set_g_stage(0) selects it); the y-row scales in d_wsc[256 …] are valid for the W image
+  // and the digit image whose largest sample exponent is g8_emax_
+  int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) != 0) ? 0 : 1;
+  bool g8_scales_ok_ = false;
+  // PICARD_G8_DBG (timing experiments only; wrong statistics): 1 = no G stage, 2 = no Y stage
+  const int g8_dbg_ = std::getenv("PICARD_G8_DBG") ? std::atoi(std::getenv("PICARD_G8_DBG")) : 0;
+  int g8_emax_ = INT_MIN;
+  uint64_t n_g8_passes_ = 0;
   bool d_wsl_ready_ = false, oz_fused_ready_ = false;
   void drop_xsl() { xsl_valid_ = false; }
   // free the slice image for good (until the next load / generate): the fp64 Y stage
@@ -3704,7 +3741,9 @@ struct DeviceCtx : Evaluator {
     pin_release(pin_wsl_);
   }
   void upload_wsl(const double* w, size_t nc) {
-    if (wsl_nc_ == nc && wsl_w_.size() == nc * nf && std::memcmp(wsl_w_.data(), w, nc * nf * sizeof(double)) == 0)
+    const int emax = xsc_range_ok_ ? xsc_emax_ : INT_MIN;
+    if (wsl_nc_ == nc && wsl_w_.size() == nc * nf && std::memcmp(wsl_w_.data(), w, nc * nf * sizeof(double)) == 0 &&
+        (nc > 128 || g8_emax_ == emax))
       return;
     // up to 16 row blocks (256 rows); k-step stride wsl_ksw() (2: the NB = 8 / 4 kernels,
     // 4: the tiled pass at nf ≤ 256); the multi-try pass puts Z in row blocks 16–31
@@ -3718,6 +3757,27 @@ struct DeviceCtx : Evaluator {
     std::memset(img, 0, img_bytes);
     for (int i = 0; i < 256; ++i) sc[i] = 0x1p-12;
     oz_split_rows(w, nc, nf, img, sc, ksw);  // host_linalg.cpp: rows split over the host threads
+    // fused_g8.inc: ysc_j = 2^(46 − F_j) with |y_jt| < 2^F_j for every sample:
+    // |y_jt| ≤ Σ_k|W_jk|·max_k|X_kt| < 2^(ilogb(Σ|W_j|) + 1)·2^emax (Σ|W_j| taken 1e-12 high for its
+    // own rounding; the digit forms of W and X and the fp64 combine stay within 2^-50 of it, and
+    // the 6-digit range reaches 0.996·2^47); zero rows (padding) get 1
+    g8_scales_ok_ = false;
+    g8_emax_ = INT_MIN;
+    if (nc <= 128 && emax != INT_MIN) {
+      bool ok = true;
+      for (size_t j = 0; j < 128; ++j) {
+        double s1 = 0.0;
+        if (j < nc)
+          for (size_t k = 0; k < nf; ++k) s1 += std::fabs(w[j * nf + k]);
+        if (!std::isfinite(s1)) { ok = false; break; }
+        if (s1 == 0.0) { sc[256 + j] = 1.0; continue; }
+        const int fj = std::ilogb(s1 * (1.0 + 1e-12)) + 1 + emax;
+        if (fj < -900 || fj > 900) { ok = false; break; }
+        sc[256 + j] = std::ldexp(1.0, 46 - fj);
+      }
+      g8_scales_ok_ = ok;
+      g8_emax_ = ok ? emax : INT_MIN;
+    }
     wsl_w_.assign(w, w + nc * nf);
     wsl_nc_ = nc;
     HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + img_bytes, hipMemcpyHostToDevice, stream));
@@ -4263,6 +4323,10 @@ struct DeviceCtx : Evaluator {
     // keep == false, or no room for Y: loss-only pass, completion recomputes the full pass.
     // With a communicator the ranks agree (once) on keeping Y: the two completions issue
     // different all-reduces.
+    // Where the fused pass may form G on int8 digits (fused_g8.inc), the completion recomputes
+    // the fused pass instead of forming G from the kept Y on fp64 MFMA: the accepted try's G then
+    // has the bits of the fused pass at its W (decided from the shape alone: rank-consistent)
+    if (g_stage_ == 0 && nb == 8 && !need_h && (d.kind == DENS_TANH || d.kind == DENS_EXP)) keep = false;
     bool store = keep && ensure_ybuf(nb);
     if (coll_ && keep) store = agree_once(ybuf_agreed_, store, "a kept Y buffer (completion from Y)");
     out->nc = nc;
@@ -4738,6 +4802,8 @@ void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int rese
     d->n_kernel = d->n_loss = d->n_fromy = d->n_split = d->n_multi = 0;
   }
 }
+void device_ctx_set_g_stage(Evaluator* e, int mode) { static_cast<DeviceCtx*>(e)->g_stage_ = mode; }
+uint64_t device_ctx_g8_passes(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_g8_passes_; }
 void device_ctx_set_y_stage(Evaluator* e, int mode) {
   auto* d = static_cast<DeviceCtx*>(e);
   d->y_stage_ = mode;

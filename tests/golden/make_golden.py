@@ -49,8 +49,25 @@ def main():
         traj[f"{tag}_n_evals"] = np.array(r.info.n_evals)
         traj[f"{tag}_amari"] = np.array(po.amari_distance(r.full_unmixing(), a))
     np.savez(os.path.join(HERE, "c1_trajectories.npz"), **traj)
+    c2_fit()
     print("wrote", sorted(os.listdir(HERE)))
 
 
+def c2_fit():
+    """BASELINE config 2 whole (64 sources × 1e6 samples of the bench mixture, seed 42),
+    Picard-O extended tanh with w_init = I: the one GPU config the oracle can fit entirely
+    (≈ a minute of numpy). tests/test_gpu_golden.py fits the same data on the device."""
+    x, _, a = datagen.generate_data(64, 1_000_000, 42)
+    r = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(64)))
+    np.savez(os.path.join(HERE, "c2_fit.npz"), n_iter=np.array(r.n_iterations), converged=np.array(r.converged),
+             unmixing=r.unmixing, whitening=r.whitening, mean=r.mean, a=a,
+             amari=np.array(po.amari_distance(r.full_unmixing(), a)),
+             loss=np.array(r.info.trace_loss), gnorm=np.array(r.info.trace_gnorm),
+             n_evals=np.array(r.info.n_evals))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["c2"]:
+        c2_fit()
+    else:
+        main()

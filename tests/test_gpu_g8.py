@@ -1,0 +1,186 @@
+"""GPU parity of the fused pass with G = ψ·Yᵀ on int8 digits (fused_g8.inc).
+
+Where the fused pass runs on the int8 digit Y stage (64 < nc ≤ 128, n_features ≤ 128, tanh or
+exp, no H), ψ and y are split into signed radix-256 digits at one fixed scale per row and pass
+and G is summed exactly in int32 per 64-sample chunk. Tolerances: G, Σψ′, Σℓ, Σy² against the
+fp64 oracle at the file-wide 1e-12 relative bound of test_gpu_parity.py; against the same
+context's fp64 G stage (pc_ctx_set_g_stage F64) the row sums are bit-identical (the Y waves are
+the same code) and G agrees to 1e-12 at T ≈ 5e3 (measured ≈ 1e-13 there) and to 1e-13 at
+T = 2^20 (the error of the fixed-point products grows as √T, G itself as T: tools/g8_emulate.py).
+Every test asserts that the digit G kernel ran (pc_ctx_g8_passes).
+"""
+import numpy as np
+import pytest
+
+from conftest import density_of, rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+TOL_MODES = 1e-13
+DENSITIES = [("tanh", 1.0), ("tanh", 0.7), ("exp", 1.0), ("exp", 0.1)]
+
+
+@pytest.fixture(scope="module")
+def rng():
+    return np.random.default_rng(8642)
+
+
+def laplace_mix(rng, nf, t):
+    s = rng.laplace(size=(nf, t))
+    a = rng.uniform(-0.5, 0.5, size=(nf, nf)) + np.eye(nf)
+    return a @ s + rng.normal(size=(nf, 1))
+
+
+def dens_of(pa, dens):
+    kind, alpha = dens
+    return pa.DensityType.tanh(alpha) if kind == "tanh" else pa.DensityType.exp(alpha)
+
+
+@pytest.mark.parametrize("n", [65, 100, 128])
+@pytest.mark.parametrize("dens", DENSITIES)
+def test_g8_vs_oracle_and_f64_g(pa, po, rng, n, dens):
+    """The fused pass with the digit G stage against the oracle (1e-12) and against the fp64
+    G stage of the same context (row sums bit-identical, G within 1e-12 at this T)."""
+    x = laplace_mix(rng, n, 5003)
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    got = ctx.eval(w, mu, d, False, need_y2=True)
+    assert ctx.g8_passes == 1
+    want = po.pass_stats(w, mu, x, density_of(po, d), False)
+    for k in want:
+        assert rel_err(got[k], want[k]) <= TOL, (k, rel_err(got[k], want[k]))
+    ctx.set_g_stage("f64")
+    ref = ctx.eval(w, mu, d, False, need_y2=True)
+    assert ctx.g8_passes == 1
+    for k in ("dpsi", "ll", "y2"):
+        assert np.array_equal(got[k], ref[k]), k
+    assert rel_err(got["G"], ref["G"]) <= TOL, rel_err(got["G"], ref["G"])
+
+
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 1.0)])
+def test_g8_vs_f64_g_large_t(pa, rng, dens):
+    """At T = 2^20 (the digit G stage runs on shards of C3's size, 1.25e7–1e8) the two G stages
+    agree to 1e-13 relative; the row sums are bit-identical."""
+    n, t = 128, 1 << 20
+    x = laplace_mix(rng, n, t)
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    got = ctx.eval(w, mu, d, False)
+    assert ctx.g8_passes == 1
+    ctx.set_g_stage("f64")
+    ref = ctx.eval(w, mu, d, False)
+    for k in ("dpsi", "ll"):
+        assert np.array_equal(got[k], ref[k]), k
+    assert rel_err(got["G"], ref["G"]) <= TOL_MODES, rel_err(got["G"], ref["G"])
+
+
+@pytest.mark.parametrize("t", [1, 15, 16, 47, 64, 65, 1000, 200_017])
+def test_g8_ragged_chunks(pa, po, rng, t):
+    """T not a multiple of the 64-sample chunk, workgroups whose last chunk is partial or
+    holds a single block, and (T = 200 017) many chunks per workgroup."""
+    n = 128
+    x = laplace_mix(rng, n, t)
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = pa.DensityType.tanh()
+    got = ctx.eval(w, mu, d, False)
+    assert ctx.g8_passes == 1
+    want = po.pass_stats(w, mu, x, density_of(po, d), False)
+    for k in want:
+        assert rel_err(got[k], want[k]) <= TOL, (k, t, rel_err(got[k], want[k]))
+
+
+def test_g8_zero_rows_and_wide_rows(pa, po, rng):
+    """A zero row of W (y = ψ = 0: its scale is 1, its digits 0), a row far below the others
+    (its own y scale) and nc < 128 (padding rows)."""
+    n, t = 100, 4099
+    x = laplace_mix(rng, n, t)
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    w[7] = 0.0
+    w[3] *= 1e-9
+    w[11] *= 1e6
+    mu = x.mean(axis=1)
+    d = pa.DensityType.tanh()
+    got = ctx.eval(w, mu, d, False)
+    assert ctx.g8_passes == 1
+    want = po.pass_stats(w, mu, x, density_of(po, d), False)
+    for k in want:
+        assert rel_err(got[k], want[k]) <= TOL, (k, rel_err(got[k], want[k]))
+    assert np.all(got["G"][7] == 0) and np.all(got["G"][:, 7] == 0)
+    # the scaled-down row's column of G (its y) carries its own scale: relative accuracy
+    assert rel_err(got["G"][:, 3], want["G"][:, 3]) <= 1e-10
+
+
+def test_g8_split_eval_bit_identical(pa, rng):
+    """Loss-only try + completion (which recomputes the fused pass on the digit G shapes)
+    gives exactly the fused pass's statistics."""
+    n, t = 128, 30011
+    x = laplace_mix(rng, n, t)
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    d = pa.DensityType.tanh()
+    full = ctx.eval(w, None, d, False, need_y2=False)
+    lo, kept, done = ctx.eval_split(w, None, d, False, need_y2=False)
+    assert kept and ctx.g8_passes == 2
+    assert np.array_equal(lo["ll"], full["ll"])
+    for k in ("G", "dpsi", "ll"):
+        assert np.array_equal(done[k], full[k]), k
+
+
+def test_g8_non_finite_falls_back(pa, rng):
+    """A NaN in X: the digit image's exponent range is unusable, so the pass keeps G on fp64
+    MFMA and the NaN reaches G and the row sums as the fp64 path gives it."""
+    n, t = 128, 2000
+    x = laplace_mix(rng, n, t)
+    x[4, 321] = np.nan
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    got = ctx.eval(w, None, pa.DensityType.tanh(), False)
+    assert ctx.g8_passes == 0
+    assert np.isnan(got["G"]).all() and np.isnan(got["ll"]).all()
+
+
+def test_g8_fit_matches_f64_g_fit(pa, rng):
+    """A Picard-O fit on the digit G stage against the same fit on the fp64 G stage: same
+    iterations ±2, unmixing within 1e-6 (G differs only by rounding)."""
+    n, t = 96, 60000
+    x = laplace_mix(rng, n, t)
+
+    def fit(mode):
+        ctx = pa.DeviceContext(0)
+        ctx.set_g_stage(mode)
+        ctx.load(x)
+        sv = pa.Solver(ctx, pa.PicardConfig(random_state=3, max_iter=200, want_sources=False))
+        while not sv.step():
+            pass
+        r = sv.finish()
+        g8 = ctx.g8_passes
+        sv.close()
+        ctx.close()
+        return r, g8
+
+    r8, n8 = fit("auto")
+    r64, n64 = fit("f64")
+    assert n8 > 0 and n64 == 0
+    assert r8.converged and r64.converged
+    assert abs(r8.n_iterations - r64.n_iterations) <= 2
+    assert np.max(np.abs(r8.unmixing - r64.unmixing)) <= 1e-6
