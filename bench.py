@@ -46,6 +46,7 @@ HBM_PEAK_GBS = 8000.0
 # "I8: 2x BF16 per clock"; 16 cycles/MFMA confirmed by SQ_VALU_MFMA_BUSY_CYCLES) at 2.4 GHz
 I8_MFMA_PEAK_TOPS = 32768 / 16 * 1024 * 2.4e9 / 1e12   # = 5033
 OZ_PRODUCTS = 28   # digit products per multiply-add of the int8-digit Y stage (ozaki.inc)
+G8_PRODUCTS = 26   # … of the int8-digit G stage (fused_g8.inc: 6 + 6 digits, diagonals qa + qb >= 4)
 OZ_SCREEN_PRODUCTS = 10   # … of the line-search screen (diagonals D <= 3; an undecided try is
                           # screened again on D <= 4, 15 products: counted at 10 here)
 
@@ -291,6 +292,7 @@ def main():
     ctx.kernel_stats(reset=True)
     ctx.kernel_breakdown(reset=True)
     int8_before = ctx.int8_passes
+    g8_before = ctx.g8_passes
     ctx.screen_stats(reset=True)
     passes = 0
     ar0 = ctx.comm_timing()
@@ -320,6 +322,7 @@ def main():
     _, call_ms, _ = ctx.kernel_stats(reset=False)
     brk = ctx.kernel_breakdown(reset=False)
     int8_timed = ctx.int8_passes - int8_before
+    g8_timed = ctx.g8_passes - g8_before
     brk["screen"] = ctx.screen_stats(reset=False)
     screen_tries = ctx.screen_tries()  # a paired pass (two tries) counts 2
 
@@ -391,7 +394,10 @@ def main():
         except Exception:
             pass
     i8 = int8_timed > 0
-    kinds = {"fused": ("k_eval_fused", "k_eval_fused_ws<tanh,noY2" + (",i8-digit Y>" if i8 else ">"), 4.0),
+    g8 = g8_timed > 0  # the fused passes formed G on int8 digits too (k_eval_fused_g8x)
+    fused_label = ("k_eval_fused_g8x<tanh,noY2> (i8-digit Y and G)" if g8 else
+                   "k_eval_fused_ws<tanh,noY2" + (",i8-digit Y>" if i8 else ">"))
+    kinds = {"fused": ("k_eval_fused", fused_label, 4.0),
              "loss": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2>" if i8 else "k_eval_loss2<tanh,nostore,noY2>", 2.0),
              "screen": ("k_screen_oz", "k_screen_oz2<NB=8> (line-search screen: D<=3 digit products, fp32 l)", 2.0)}
     rooflines = []
@@ -403,9 +409,12 @@ def main():
         flops = c * n * n * t_local
         bytes_alg = 8.0 * n * t_local
         tf = flops / (avg * 1e-3) / 1e12
-        if i8:  # executed: Y stage as i8 digit products, G (fused only) on fp64 MFMA
+        if i8:  # executed: Y stage as i8 digit products, G (fused only) on fp64 MFMA or i8 digits
             i8_ops = (OZ_SCREEN_PRODUCTS if kind == "screen" else OZ_PRODUCTS) * 2.0 * n * n * t_local
             f64_ops = flops - 2.0 * n * n * t_local
+            if kind == "fused" and g8:
+                i8_ops += G8_PRODUCTS * 2.0 * n * n * t_local
+                f64_ops = 0.0
             ideal_s = i8_ops / (I8_MFMA_PEAK_TOPS * 1e12) + f64_ops / (FP64_MFMA_PEAK_TFLOPS * 1e12)
             peak = flops / ideal_s / 1e12
             executed = {"i8_ops_per_launch": i8_ops, "fp64_mfma_flops_per_launch": f64_ops,
@@ -442,7 +451,10 @@ def main():
         "metric": "samples/sec per Picard-O iter at N=128, T=1e8; iters to tol=1e-7",
         "value": value, "unit": "samples/s per iteration", "n_gpus": world, "steps": steps_run,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f64" + (" (Y = W·X from exact i8 digit products)" if i8 else ""), "data": "synthetic (benches/benchmarks.rs LCG mixture, seed 42, in HBM)",
+        "vs_baseline": None, "dtype": "f64" + ((" (Y = W·X from exact i8 digit products; G = ψ·Yᵀ from i8 digit "
+                                                "products summed exactly per 64 samples, within 1e-13 of fp64 "
+                                                "at this size)") if g8 else (" (Y = W·X from exact i8 digit products)"
+                                                                              if i8 else "")), "data": "synthetic (benches/benchmarks.rs LCG mixture, seed 42, in HBM)",
         "config": {"workload": f"Picard-O extended tanh, N={n} sources, T={T} samples (BASELINE configs[2])",
                    "n_sources": n, "n_samples": T, "ortho": True, "extended": True, "density": "tanh(1)",
                    "parallelism": f"T-sharded over {world} GPU(s), RCCL all-reduce of stats per pass",
@@ -452,6 +464,7 @@ def main():
                                    "every try exactly: tests/test_gpu_int8.py); screens run inside the timed "
                                    "region and are counted in screen_passes_per_iter") if i8 else "every try exact"},
         "passes_per_iter": passes / steps, "screen_passes_per_iter": brk["screen"][1] / steps,
+        "g8_passes_per_iter": g8_timed / steps,
         "screened_tries_per_iter": screen_tries / steps,
         "iters_to_tol": iters_to_tol, "converged": converged,
         "total_passes_to_tol": total_passes,

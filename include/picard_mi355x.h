@@ -372,14 +372,15 @@ enum { PC_YSTAGE_AUTO = 0, PC_YSTAGE_F64 = 1, PC_YSTAGE_INT8_EXACT = 2 };
 int pc_ctx_set_y_stage(pc_ctx* ctx, int32_t mode);
 /* number of passes whose Y stage ran on the int8 slices since the context was created */
 uint64_t pc_ctx_int8_passes(const pc_ctx* ctx);
-/* G-stage arithmetic of the orthogonal fused pass (G = ψ(Y)·Yᵀ, core.rs:218). PC_GSTAGE_AUTO:
+/* G-stage arithmetic of the orthogonal fused pass (G = ψ(Y)·Yᵀ, core.rs:218). PC_GSTAGE_AUTO
+ * (default):
  * where the fused pass runs on the int8 digit Y stage (64 < nc ≤ 128, nf ≤ 128, tanh or exp),
  * ψ and y are also split into 6 signed radix-256 digits each at one fixed scale per row and
  * pass, and G is summed exactly in int32 per 64-sample chunk on the i8 matrix cores (the 26
  * leading digit products), then in fp64 (G within 1e-13 of the fp64 stage at
- * T ≥ 2^20, 1e-12 at T ≈ 5e3). PC_GSTAGE_F64 (default): G on the fp64 MFMA. Row sums (Σψ′, Σℓ,
- * Σy²) are bit-identical in both modes. (PICARD_G8=1 in the environment selects
- * PC_GSTAGE_AUTO for new contexts.) */
+ * T ≥ 2^20, 1e-12 at T ≈ 5e3). PC_GSTAGE_F64: G on the fp64 MFMA. Row sums (Σψ′, Σℓ, Σy²)
+ * are bit-identical in both modes. (PICARD_G8=0 in the environment selects PC_GSTAGE_F64 for
+ * new contexts.) */
 enum { PC_GSTAGE_AUTO = 0, PC_GSTAGE_F64 = 1 };
 int pc_ctx_set_g_stage(pc_ctx* ctx, int32_t mode);
 /* number of fused passes whose G stage ran on int8 digits since the context was created */

@@ -878,6 +878,7 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 // ---------------------------------------------------------------------------
 #include "fused_ws.inc"
 #include "fused_g8.inc"  // the same pass with G = ψ·Yᵀ on int8 digits too
+#include "fused_g8x.inc"  // … the same arithmetic, 8 waves, G interleaved with the Y stage
 
 // ---------------------------------------------------------------------------
 // Split evaluation for line-search tries (bit-identical sums to k_eval_fused):
@@ -3005,10 +3006,18 @@ struct DeviceCtx : Evaluator {
           const double bound = 1.0 / std::sqrt(alpha * 2.718281828459045) * (1.0 + 1e-12);
           psc = std::ldexp(1.0, 46 - (std::ilogb(bound) + 1));
         }
-        auto kg8 = k_eval_fused_g8<D, Q>;
-        lds_attr((const void*)kg8, G8_LDS);
         HIP_OK(hipEventRecord(ev[1], stream));
-        kg8<<<nwg, WS_THREADS, G8_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc, g8_dbg_);
+        if (g8_phased_) {  // PICARD_G8_PHASED=1: the role-specialised phased kernel
+          auto kg8 = k_eval_fused_g8<D, Q>;
+          lds_attr((const void*)kg8, G8_LDS);
+          HIP_OK(hipEventRecord(ev[1], stream));
+          kg8<<<nwg, WS_THREADS, G8_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc, g8_dbg_);
+        } else {
+          auto kg8x = k_eval_fused_g8x<D, Q>;
+          lds_attr((const void*)kg8x, G8X_LDS);
+          HIP_OK(hipEventRecord(ev[1], stream));
+          kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
+        }
         HIP_OK(hipGetLastError());
         ++n_int8_passes_;
         ++n_g8_passes_;
@@ -3582,14 +3591,15 @@ struct DeviceCtx : Evaluator {
   double* d_wsc = nullptr;
   int y_stage_ = 0;
   uint64_t n_int8_passes_ = 0;
-  // G = ψ·Yᵀ on int8 digits (fused_g8.inc): g_stage_ 0 = where the shape allows, 1 = the fp64 G
-  // stage (the default until the digit stage is the faster one; PICARD_G8=1 or
-  // pc_ctx_set_g_stage(0) selects it); the y-row scales in d_wsc[256 …] are valid for the W image
-  // and the digit image whose largest sample exponent is g8_emax_
-  int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) != 0) ? 0 : 1;
+  // G = ψ·Yᵀ on int8 digits (fused_g8.inc, fused_g8x.inc): g_stage_ 0 = where the shape allows
+  // (default), 1 = the fp64 G stage (PICARD_G8=0 or pc_ctx_set_g_stage(1)); the y-row scales in
+  // d_wsc[256 …] are valid for the W image and the digit image whose largest sample exponent is
+  // g8_emax_
+  int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) == 0) ? 1 : 0;
   bool g8_scales_ok_ = false;
   // PICARD_G8_DBG (timing experiments only; wrong statistics): 1 = no G stage, 2 = no Y stage
   const int g8_dbg_ = std::getenv("PICARD_G8_DBG") ? std::atoi(std::getenv("PICARD_G8_DBG")) : 0;
+  const bool g8_phased_ = std::getenv("PICARD_G8_PHASED") && std::atoi(std::getenv("PICARD_G8_PHASED")) != 0;
   int g8_emax_ = INT_MIN;
   uint64_t n_g8_passes_ = 0;
   bool d_wsl_ready_ = false, oz_fused_ready_ = false;

@@ -244,6 +244,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   trace_ = std::getenv("PICARD_TRACE") != nullptr;
   keep_y_ = std::getenv("PICARD_KEEP_Y") != nullptr;
   no_multi_ = std::getenv("PICARD_NO_MULTI") != nullptr;
+  if (const char* e = std::getenv("PICARD_MULTI_GROUP")) multi_group_ = (size_t)std::max(0, std::atoi(e));
   split_first_ = std::getenv("PICARD_SPLIT_FIRST") != nullptr;
   init_core();
   lap(4);
@@ -576,72 +577,89 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         bounded = ev_->eval_loss_multi_bound(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
                                              alphas.data(), (int)na, ll.data(), bnd.data());
       }
+      // Staged tries (exact path; schedule only): the pass's cost grows with its tries (each is
+      // a density evaluation per element), and a search is usually decided by an early try, so
+      // the first pass covers the first multi_group_ tries and a second pass the rest only if
+      // none of them is accepted. Each try's sums do not depend on which others share its pass
+      // (k_multi_loss2*: per-try accumulators, the same arithmetic per try), so every decision
+      // is the one-pass schedule's.
+      const size_t g1 = bounded || multi_group_ == 0 ? na : std::min(na, multi_group_);
+      size_t j0 = 0, nj = g1;
       if (bounded || ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
-                                          alphas.data(), (int)na, ll.data(), y2.data())) {
-        ++last_evals_;
-        ++total_evals_;
+                                          alphas.data(), (int)nj, ll.data(), y2.data())) {
         EvalStats ls;
         ls.nc = n;
         ls.has_h = false;
         ls.buf.assign(EvalStats::size(n, false), 0.0);
-        // every try's W_j = (I + α_j D)·W and log|det W_j| (core.rs:124-125, :43-47),
-        // formed for all tries at once on the host threads; each is the same serial
-        // arithmetic as in the walk below, which then accepts in the reference order
         std::vector<Mat> wj(na);
         std::vector<double> dsg(na), dla(na);
         wj[0] = r.w;
-#pragma omp parallel for schedule(dynamic, 1) if (na > 1)
-        for (size_t j = 0; j < na; ++j) {
-          if (j > 0) {
-            Mat tj = Mat::eye(n);
-            for (size_t e = 0; e < tj.a.size(); ++e) tj.a[e] += alphas[j] * direction.a[e];
-            wj[j] = matmul(tj, W_);
-          }
-          sln_det(wj[j], &dsg[j], &dla[j]);
-        }
         EvalStats last_full;  // bounded: the exact pass of the LAST try, if one ran and rejected it
         bool have_last_full = false;
-        for (size_t j = 0; j < na; ++j) {
-          const double a = alphas[j];
-          r.w = std::move(wj[j]);
-          std::memcpy(const_cast<double*>(ls.ll()), ll.data() + j * n, n * sizeof(double));
-          std::memcpy(const_cast<double*>(ls.y2()), y2.data() + j * n, n * sizeof(double));
-          r.tries = k + j + 1;
-          bool singular;
-          const double loss = loss_of(ls, r.w, signs_, &singular, dsg[j], dla[j]);
-          if (bounded) {
-            // core.rs:127-140 on the exact loss: a try whose lower bound cannot beat the
-            // current loss fails; the first one that might is evaluated in full (that pass is
-            // the new iterate if it is accepted) and decided on its exact loss
-            double eb = 0.0;
-            for (size_t i = 0; i < n; ++i) eb += std::fabs(signs_[i]) * bnd[j * n + i] / (double)T_;
-            if (!singular && loss - eb < current_loss_) {
-              EvalStats full;
-              evaluate(r.w, &full);
-              const double exact = loss_of(full, r.w, signs_, &singular, dsg[j], dla[j]);
-              if (exact < current_loss_) {
-                r.stats = std::move(full);
-                r.partial = false;
-                r.loss = exact;
-                r.success = true;
-                r.step = scale(direction, a);
-                return r;
-              }
-              multi_bound_on_ = false;  // a full pass spent on a rejected try: exact tries from now on
-              if (j + 1 == na) {  // kept below: step() needs no second pass at the same W
-                last_full = std::move(full);
-                have_last_full = true;
-              }
+        for (;;) {  // one pass over tries j0 … j0 + nj − 1
+          ++last_evals_;
+          ++total_evals_;
+          // every try's W_j = (I + α_j D)·W and log|det W_j| (core.rs:124-125, :43-47),
+          // formed for the pass's tries at once on the host threads; each is the same serial
+          // arithmetic as in the walk below, which then accepts in the reference order
+#pragma omp parallel for schedule(dynamic, 1) if (nj > 1)
+          for (size_t j = j0; j < j0 + nj; ++j) {
+            if (j > 0) {
+              Mat tj = Mat::eye(n);
+              for (size_t e = 0; e < tj.a.size(); ++e) tj.a[e] += alphas[j] * direction.a[e];
+              wj[j] = matmul(tj, W_);
             }
-          } else if (loss < current_loss_) {
-            evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
-            r.partial = false;
-            r.loss = loss_of(r.stats, r.w, signs_, &singular);
-            r.success = true;
-            r.step = scale(direction, a);
-            return r;
+            sln_det(wj[j], &dsg[j], &dla[j]);
           }
-          alpha = a / 2.0;
+          for (size_t j = j0; j < j0 + nj; ++j) {
+            const double a = alphas[j];
+            r.w = std::move(wj[j]);
+            std::memcpy(const_cast<double*>(ls.ll()), ll.data() + j * n, n * sizeof(double));
+            std::memcpy(const_cast<double*>(ls.y2()), y2.data() + j * n, n * sizeof(double));
+            r.tries = k + j + 1;
+            bool singular;
+            const double loss = loss_of(ls, r.w, signs_, &singular, dsg[j], dla[j]);
+            if (bounded) {
+              // core.rs:127-140 on the exact loss: a try whose lower bound cannot beat the
+              // current loss fails; the first one that might is evaluated in full (that pass is
+              // the new iterate if it is accepted) and decided on its exact loss
+              double eb = 0.0;
+              for (size_t i = 0; i < n; ++i) eb += std::fabs(signs_[i]) * bnd[j * n + i] / (double)T_;
+              if (!singular && loss - eb < current_loss_) {
+                EvalStats full;
+                evaluate(r.w, &full);
+                const double exact = loss_of(full, r.w, signs_, &singular, dsg[j], dla[j]);
+                if (exact < current_loss_) {
+                  r.stats = std::move(full);
+                  r.partial = false;
+                  r.loss = exact;
+                  r.success = true;
+                  r.step = scale(direction, a);
+                  return r;
+                }
+                multi_bound_on_ = false;  // a full pass spent on a rejected try: exact tries from now on
+                if (j + 1 == na) {  // kept below: step() needs no second pass at the same W
+                  last_full = std::move(full);
+                  have_last_full = true;
+                }
+              }
+            } else if (loss < current_loss_) {
+              evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
+              r.partial = false;
+              r.loss = loss_of(r.stats, r.w, signs_, &singular);
+              r.success = true;
+              r.step = scale(direction, a);
+              return r;
+            }
+            alpha = a / 2.0;
+          }
+          j0 += nj;
+          if (j0 >= na) break;
+          nj = na - j0;  // the remaining tries in one more pass
+          ++multi_second_passes_;
+          if (!ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
+                                    alphas.data() + j0, (int)nj, ll.data() + j0 * n, y2.data() + j0 * n))
+            throw computation_error("multi-try pass refused after an earlier one ran");
         }
         // no try accepted: the caller evaluates the last try in full if it keeps it — unless
         // the bounded path already ran that pass (its exact statistics and loss are kept)

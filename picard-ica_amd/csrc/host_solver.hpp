@@ -128,6 +128,10 @@ class Solver {
   Mat C1_;
   double ls_slope_ = 0.0, ls_curv_ = 0.0, ls_q_ = 0.0, ls_k3_ = 0.0, ls_slack_ = 0.0;
   uint64_t curv_skips_ = 0;
+  // non-orthogonal searches: tries in the first multi-try pass (0: all; PICARD_MULTI_GROUP)
+  // and how many searches needed a second pass for the rest
+  size_t multi_group_ = 0;
+  uint64_t multi_second_passes_ = 0;
   void set_curvature(const Mat& g, const Mat& gs, const Mat& d, double slope);
   double curvature_lower_bound(double alpha) const;
   // first-try policy: outcomes of descent-direction first tries

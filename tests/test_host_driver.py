@@ -264,3 +264,42 @@ def test_model_schedule_decisions_unchanged(pa, po, dg, n, t, seed, capfd, monke
     assert "[picard-model]" in err and "[picard-pred]" in err
     assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
     assert np.array_equal(r1.unmixing, r0.unmixing)
+
+
+@pytest.mark.parametrize("group", [1, 3])
+def test_staged_multi_try_decisions_unchanged(pa, po, dg, group, monkeypatch):
+    """Non-orthogonal searches with the tries split over two multi-try passes (the first covers
+    `group` tries, PICARD_MULTI_GROUP) decide exactly as with all tries in one pass: each try's
+    sums do not depend on the pass that carries it. Counts the passes to show the split ran."""
+    x, _ = dg.generate_data(12, 8000, 42)[:2]
+    calls = []
+
+    def ev(w, mu, d, need_h):
+        return po.pass_stats(w, mu, x, density_of(po, d), need_h)
+
+    def multi(w, z, alphas, mu, d):
+        calls.append(len(alphas))
+        ll, y2 = [], []
+        for a in alphas:
+            st = po.pass_stats(w + a * z, mu, x, density_of(po, d), False)
+            ll.append(st["ll"])
+            y2.append(st["y2"])
+        return np.array(ll), np.array(y2)
+
+    def fit():
+        calls.clear()
+        r = pa.fit_with_host_evaluator(
+            x.shape[0], x.shape[1], pa.PicardConfig(ortho=False, extended=False, random_state=7, max_iter=80),
+            rowsum=lambda: x.sum(axis=1), gram=lambda mu: (x - mu[:, None]) @ (x - mu[:, None]).T,
+            eval=ev, sources=lambda w, mu: w @ (x - mu[:, None]), eval_loss_multi=multi)
+        return r, list(calls)
+
+    monkeypatch.delenv("PICARD_MULTI_GROUP", raising=False)
+    r0, c0 = fit()
+    monkeypatch.setenv("PICARD_MULTI_GROUP", str(group))
+    r1, c1 = fit()
+    assert c0 and max(c0) > group  # one pass per search carried more than `group` tries
+    assert max(c1[i] for i in range(len(c1))) >= 1 and all(n <= max(c0) for n in c1)
+    assert any(n == group for n in c1)  # first passes capped at `group` tries
+    assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
+    assert np.array_equal(r1.unmixing, r0.unmixing)
