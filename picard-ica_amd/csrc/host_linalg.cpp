@@ -431,6 +431,17 @@ bool sym_decorrelation(const Mat& w, Mat* out) {
   return true;
 }
 
+static double norm_inf(const Mat& m) {  // max row sum (contiguous rows)
+  double r = 0.0;
+  for (size_t i = 0; i < m.rows; ++i) {
+    const double* p = m.data() + i * m.cols;
+    double s = 0.0;
+    for (size_t j = 0; j < m.cols; ++j) s += std::fabs(p[j]);
+    r = std::fmax(r, s);
+  }
+  return r;
+}
+
 Mat matrix_exp(const Mat& a) {
   const size_t n = a.rows;
   const double norm = max_abs(a);
@@ -439,6 +450,87 @@ Mat matrix_exp(const Mat& a) {
   const double sc = std::ldexp(1.0, s);
   Mat as = a;
   for (double& v : as.a) v /= sc;
+  // math.rs:38-74 sums the series term by term until max|term| < 1e-16 (at most 30 terms), then
+  // squares s times. Where that series converges within its 30 terms it is exp(as) to rounding,
+  // and the same value comes from far fewer products (Paterson–Stockmeyer):
+  // * the powers B^1 … B^4 of B = as (3 products) and their ∞-norms ν_k bound every power,
+  //   ‖B^k‖ ≤ ν_4^⌊k/4⌋·ν_(k mod 4) — for the skew-symmetric directions of the orthogonal
+  //   search (normal matrices) ν_4^(1/4) is close to the spectral radius, far below ‖B‖;
+  // * the series converged if Σ_{k>30} ‖B^k‖/k! < 1e-17 by that bound; otherwise the reference
+  //   stops at its 30-term cap short of exp(as), and the term-by-term loop below restates that
+  //   truncated value;
+  // * else halve B t more times (its powers scale exactly by 2^-kt) and pick the degree m whose
+  //   remainder bound is below 1e-17, (t, m) minimising ⌊m/4⌋ + t products: a Horner recursion
+  //   in B^4 over blocks Σ_{i<4} B^i/(4j+i)!, then s + t squarings. The powers of two 2^-it are
+  //   folded into the block coefficients and the Horner step (exact).
+  std::vector<Mat> pw(5);
+  pw[1] = as;
+  double nu[5] = {1.0, norm_inf(as), 0.0, 0.0, 0.0};
+  for (int k = 2; k <= 4; ++k) {
+    pw[k] = matmul(pw[k - 1], as);
+    nu[k] = norm_inf(pw[k]);
+  }
+  // tails[t][m] = Σ_{k>m} bound(k)/k! at scale 2^-t (terms beyond k = 90 are negligible here)
+  constexpr int KMAX = 90, TMAX = 6;
+  double tails[TMAX + 1][32];
+  for (int t = 0; t <= TMAX; ++t) {
+    const double f = std::ldexp(1.0, -t);
+    const double fr[4] = {1.0, f, f * f, f * f * f};
+    const double b4 = nu[4] * fr[2] * fr[2];
+    double term[KMAX + 1] = {};
+    double inv_fact = 1.0, p4 = 1.0;
+    for (int k = 1; k <= KMAX; ++k) {
+      inv_fact /= (double)k;
+      if (k % 4 == 0) p4 *= b4;
+      term[k] = p4 * nu[k % 4] * fr[k % 4] * inv_fact;
+      if (k % 4 == 3 && p4 * inv_fact < 1e-250) break;  // the rest is negligible (and no subnormals)
+    }
+    double sum = 0.0;
+    for (int k = KMAX; k > 31; --k) sum += term[k];
+    for (int m = 31; m >= 0; --m) {
+      tails[t][m] = sum;
+      if (m > 0) sum += term[m];
+    }
+  }
+  if (std::isfinite(nu[4]) && tails[0][30] < 1e-17) {
+    int t = 0, m = 30, best_cost = 1 << 30;
+    for (int tt = 0; tt <= TMAX; ++tt)
+      for (int mm = 1; mm <= 30; ++mm)
+        if (tails[tt][mm] < 1e-17) {
+          if (mm / 4 + tt < best_cost) best_cost = mm / 4 + tt, t = tt, m = mm;
+          break;
+        }
+    // B̃ = 2^-t·B: B̃^(4j+i) = (f4·B^4)^j·f^i·B^i, so R_nb = block_nb and R_j = R_(j+1)·(f4·B^4) +
+    // block_j with block_j = Σ_{i<4, 4j+i ≤ m} f^i/(4j+i)!·B^i (B^0 = I)
+    const double f = std::ldexp(1.0, -t), f4 = std::ldexp(1.0, -4 * t);
+    std::vector<double> cf(m + 1);  // 1/k!
+    cf[0] = 1.0;
+    for (int k = 1; k <= m; ++k) cf[k] = cf[k - 1] / (double)k;
+    // R ← g·R + block_j in one sweep (g = f4 after a Horner product, else 1)
+    auto add_block = [&](Mat& r, int j, double g) {
+      double ci[4] = {0.0, 0.0, 0.0, 0.0}, fi = 1.0;
+      for (int i = 0; i < 4 && 4 * j + i <= m; ++i, fi *= f) ci[i] = cf[4 * j + i] * fi;
+      double* o = r.data();
+      const double *p1 = pw[1].data(), *p2 = pw[2].data(), *p3 = pw[3].data();
+      for (size_t e = 0; e < n * n; ++e) o[e] = g * o[e] + (ci[1] * p1[e] + ci[2] * p2[e] + ci[3] * p3[e]);
+      for (size_t d = 0; d < n; ++d) o[d * n + d] += ci[0];
+    };
+    const int nb = m / 4;
+    Mat result(n, n);
+    int j = nb;
+    if (m % 4 == 0) {  // the top block is cf[m]·I: R_(nb−1) = cf[m]·f4·B^4 + block_(nb−1), no product
+      const double top = cf[m] * f4;
+      for (size_t e = 0; e < n * n; ++e) result.a[e] = top * pw[4].a[e];
+      --j;
+    }
+    add_block(result, j, 1.0);
+    for (--j; j >= 0; --j) {
+      result = matmul(result, pw[4]);
+      add_block(result, j, f4);
+    }
+    for (int i = 0; i < s + t; ++i) result = matmul(result, result);
+    return result;
+  }
   Mat result = Mat::eye(n), term = Mat::eye(n);
   for (int k = 1; k <= 30; ++k) {
     term = matmul(term, as);
