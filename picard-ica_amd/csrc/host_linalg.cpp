@@ -193,8 +193,23 @@ double max_abs(const Mat& a) {
 }
 
 double dot_sum(const Mat& a, const Mat& b) {
+  // (a * b).sum() of the reference: ndarray sums a contiguous array in 8 interleaved partial
+  // sums (numeric_util::unrolled_fold), combined as ((((0 + (p0+p4)) + (p1+p5)) + (p2+p6)) +
+  // (p3+p7)), then the < 8 remaining elements in order. Eight independent chains instead of one
+  // dependent add per element (the L-BFGS recursion takes 2m of these per iteration).
+  const double* x = a.data();
+  const double* y = b.data();
+  const size_t n = a.a.size();
+  double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    for (int j = 0; j < 8; ++j) p[j] += x[i + j] * y[i + j];
   double s = 0.0;
-  for (size_t i = 0; i < a.a.size(); ++i) s += a.a[i] * b.a[i];
+  s = s + (p[0] + p[4]);
+  s = s + (p[1] + p[5]);
+  s = s + (p[2] + p[6]);
+  s = s + (p[3] + p[7]);
+  for (; i < n; ++i) s += x[i] * y[i];
   return s;
 }
 

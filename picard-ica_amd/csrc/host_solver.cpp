@@ -21,6 +21,7 @@
 #include <omp.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/resource.h>
 #include <thread>
 
 namespace pcamd {
@@ -476,6 +477,12 @@ class TransformWorker {
  private:
   const int nthreads_;
   void run() {
+    // below the driving thread's priority: woken by submit() right after try 1's map, a helper of
+    // equal weight was often placed on the driving thread's core and ran its whole job (all the
+    // later tries' maps) before the driver could launch try 1's pass — 0.8–1.2 ms of host time in
+    // about half the iterations of a traced N = 64 fit on the 8-core container; at nice +10 the
+    // driver keeps its core (Linux: setpriority on PRIO_PROCESS 0 applies to the calling thread)
+    setpriority(PRIO_PROCESS, 0, 10);
     omp_set_num_threads(nthreads_);
     uint64_t done_gen = 0;
     std::unique_lock<std::mutex> lk(mu_);
@@ -941,7 +948,9 @@ bool Solver::step() {
     current_loss_ = loss_of(S_, W_, signs_, &singular);
     mem_.clear();
   }
+  const double t_grad = now_ms();
   Mat direction = compute_direction(g, h, h_off, mem_, ortho);  // core.rs:334
+  const double t_dir = now_ms();
   // non-ortho: all tries in one multi-α pass unless the last search accepted at try 1
   // Schedule only (never a decision): the first try's pass also yields the next
   // gradient if it is accepted, so it is a full fused pass — unless the search
@@ -950,6 +959,7 @@ bool Solver::step() {
   // the wasted G stage. An accepted try is completed either way.
   const double slope = dot_sum(g, direction);
   set_curvature(g, gs, direction, slope);
+  const double t_curv = now_ms();
   // First-try policy cell (schedule only): Picard's quadratic model along D, L(α) − L(0) ≈
   // α·slope + α²·qh/2 with qh = Σ h_ij·D_ij² (the Hessian approximation that preconditions D),
   // predicts a decrease at α = 1 when slope + qh/2 < 0 — exactly −slope/2 for the plain Newton
@@ -968,7 +978,9 @@ bool Solver::step() {
       std::fprintf(stderr, "[picard-pred] iter %zu slope %.6e qh %.6e model %.3e first_full %d cell %d\n", iter_ + 1, slope,
                    qh, slope + 0.5 * qh, first_full_ ? 1 : 0, first_cell_);
   }
+  const double t_ls0 = now_ms(), e_ls0 = eval_ms_;
   LsResult res = line_search(direction, cfg_.ls_tries, !first_full_, ortho && slope >= 0.0);
+  const double ls_host = (now_ms() - t_ls0) - (eval_ms_ - e_ls0);
   const size_t first_tries = res.tries;
   const bool first_ok = res.success;
   first_full_ = res.success && res.tries == 1;
@@ -992,6 +1004,8 @@ bool Solver::step() {
   }
   if (trace_) {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;
+    std::fprintf(stderr, "[picard-host] iter %zu grad_ms %.3f dir_ms %.3f curv_ms %.3f ls_host_ms %.3f\n", iter_ + 1,
+                 t_grad - step_t0, t_dir - t_grad, t_curv - t_dir, ls_host);
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
                  " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f map_wait_ms %.3f screens %llu rejected %llu"
                  " curv_skips %llu screen_pairs %llu\n",
