@@ -46,7 +46,7 @@ HBM_PEAK_GBS = 8000.0
 # "I8: 2x BF16 per clock"; 16 cycles/MFMA confirmed by SQ_VALU_MFMA_BUSY_CYCLES) at 2.4 GHz
 I8_MFMA_PEAK_TOPS = 32768 / 16 * 1024 * 2.4e9 / 1e12   # = 5033
 OZ_PRODUCTS = 28   # digit products per multiply-add of the int8-digit Y stage (ozaki.inc)
-G8_PRODUCTS = 26   # … of the int8-digit G stage (fused_g8.inc: 6 + 6 digits, diagonals qa + qb >= 4)
+G8_PRODUCTS = 21   # … of the int8-digit G stage for tanh (fused_g8.inc: 6 + 6 digits, diagonals qa + qb >= 5)
 OZ_SCREEN_PRODUCTS = 10   # … of the line-search screen (diagonals D <= 3; an undecided try is
                           # screened again on D <= 4, 15 products: counted at 10 here)
 

@@ -376,8 +376,8 @@ uint64_t pc_ctx_int8_passes(const pc_ctx* ctx);
  * (default):
  * where the fused pass runs on the int8 digit Y stage (64 < nc ≤ 128, nf ≤ 128, tanh or exp),
  * ψ and y are also split into 6 signed radix-256 digits each at one fixed scale per row and
- * pass, and G is summed exactly in int32 per 64-sample chunk on the i8 matrix cores (the 26
- * leading digit products), then in fp64 (G within 1e-13 of the fp64 stage at
+ * pass, and G is summed exactly in int32 per 64-sample chunk on the i8 matrix cores (the 21
+ * leading digit products for tanh, 26 for exp), then in fp64 (G within 1e-13 of the fp64 stage at
  * T ≥ 2^20, 1e-12 at T ≈ 5e3). PC_GSTAGE_F64: G on the fp64 MFMA. Row sums (Σψ′, Σℓ, Σy²)
  * are bit-identical in both modes. (PICARD_G8=0 in the environment selects PC_GSTAGE_F64 for
  * new contexts.) */

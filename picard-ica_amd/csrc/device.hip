@@ -877,8 +877,8 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 // formulas as k_eval_fused<8> / k_eval_loss<8> / k_eval_fromy<8>: identical sums.
 // ---------------------------------------------------------------------------
 #include "fused_ws.inc"
-#include "fused_g8.inc"  // the same pass with G = ψ·Yᵀ on int8 digits too
-#include "fused_g8x.inc"  // … the same arithmetic, 8 waves, G interleaved with the Y stage
+#include "fused_g8.inc"   // G = ψ·Yᵀ on int8 digits: the arithmetic
+#include "fused_g8x.inc"  // … and the kernel (8 waves, G interleaved with the Y stage)
 
 // ---------------------------------------------------------------------------
 // Split evaluation for line-search tries (bit-identical sums to k_eval_fused):
@@ -3006,18 +3006,10 @@ struct DeviceCtx : Evaluator {
           const double bound = 1.0 / std::sqrt(alpha * 2.718281828459045) * (1.0 + 1e-12);
           psc = std::ldexp(1.0, 46 - (std::ilogb(bound) + 1));
         }
+        auto kg8x = k_eval_fused_g8x<D, Q>;
+        lds_attr((const void*)kg8x, G8X_LDS);
         HIP_OK(hipEventRecord(ev[1], stream));
-        if (g8_phased_) {  // PICARD_G8_PHASED=1: the role-specialised phased kernel
-          auto kg8 = k_eval_fused_g8<D, Q>;
-          lds_attr((const void*)kg8, G8_LDS);
-          HIP_OK(hipEventRecord(ev[1], stream));
-          kg8<<<nwg, WS_THREADS, G8_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc, g8_dbg_);
-        } else {
-          auto kg8x = k_eval_fused_g8x<D, Q>;
-          lds_attr((const void*)kg8x, G8X_LDS);
-          HIP_OK(hipEventRecord(ev[1], stream));
-          kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
-        }
+        kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
         HIP_OK(hipGetLastError());
         ++n_int8_passes_;
         ++n_g8_passes_;
@@ -3597,9 +3589,7 @@ struct DeviceCtx : Evaluator {
   // g8_emax_
   int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) == 0) ? 1 : 0;
   bool g8_scales_ok_ = false;
-  // PICARD_G8_DBG (timing experiments only; wrong statistics): 1 = no G stage, 2 = no Y stage
-  const int g8_dbg_ = std::getenv("PICARD_G8_DBG") ? std::atoi(std::getenv("PICARD_G8_DBG")) : 0;
-  const bool g8_phased_ = std::getenv("PICARD_G8_PHASED") && std::atoi(std::getenv("PICARD_G8_PHASED")) != 0;
+
   int g8_emax_ = INT_MIN;
   uint64_t n_g8_passes_ = 0;
   bool d_wsl_ready_ = false, oz_fused_ready_ = false;
