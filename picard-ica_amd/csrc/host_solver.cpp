@@ -546,9 +546,8 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
     Mat transform;
     if (ortho) {
       if (k == 0) {
-        const double tm = now_ms();
-        r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
-        map1_ms_ = now_ms() - tm;
+        // the helper starts on try 2's map while this thread forms try 1's: a paired screen
+        // needs both at once (it waited 0.33–0.41 ms for try 2's map when submitted after)
         if (tries > 1) {
           if (!ahead_) {
             ahead_.reset(new TransformWorker());
@@ -560,6 +559,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           }
           ahead_->submit(direction, W_, tries);
         }
+        const double tm = now_ms();
+        r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
+        map1_ms_ = now_ms() - tm;
       } else {
         r.w = ahead_->get(k, &ahead_wait_ms_);
       }
@@ -579,6 +581,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       // without Σy² in the loss (not extended), the tries may come with a bound instead of
       // exact sums (fp32 row terms); every decision is then taken on exact values (below)
       bool bounded = false;
+      const double tmp0 = now_ms();
       if (!extended_ && multi_bound_on_) {
         bnd.assign(na * n, 0.0);
         bounded = ev_->eval_loss_multi_bound(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
@@ -592,8 +595,10 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       // is the one-pass schedule's.
       const size_t g1 = bounded || multi_group_ == 0 ? na : std::min(na, multi_group_);
       size_t j0 = 0, nj = g1;
-      if (bounded || ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
-                                          alphas.data(), (int)nj, ll.data(), y2.data())) {
+      const bool multi_ran = bounded || ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr,
+                                                             cfg_.density, alphas.data(), (int)nj, ll.data(), y2.data());
+      eval_ms_ += now_ms() - tmp0;  // the multi-try pass is device time
+      if (multi_ran) {
         EvalStats ls;
         ls.nc = n;
         ls.has_h = false;
@@ -664,9 +669,11 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           if (j0 >= na) break;
           nj = na - j0;  // the remaining tries in one more pass
           ++multi_second_passes_;
+          const double tmp1 = now_ms();
           if (!ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
                                     alphas.data() + j0, (int)nj, ll.data() + j0 * n, y2.data() + j0 * n))
             throw computation_error("multi-try pass refused after an earlier one ran");
+          eval_ms_ += now_ms() - tmp1;
         }
         // no try accepted: the caller evaluates the last try in full if it keeps it — unless
         // the bounded path already ran that pass (its exact statistics and loss are kept)
@@ -800,8 +807,10 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         // undecided, but the estimate lies above the current loss (a likely rejection): the
         // finer screen first, when the evaluator has one, before the full pass. Its inputs
         // are the reduced statistics, so every rank takes the same branch.
+        const double tf = now_ms();
         if (!rejected && lo + eb > current_loss_ &&
             ev_->eval_loss_screen_fine(wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) {
+          eval_ms_ += now_ms() - tf;  // device time (host_ms counted it before round 5)
           ++screen_passes_;
           lo = 0.0;
           eb = 0.0;

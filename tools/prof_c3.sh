@@ -1,4 +1,4 @@
-# usage: bash tools/prof_r04i.sh TAG — round-4 C3 profile set under gpurun_out/prof_TAG/:
+# usage: bash tools/prof_c3.sh TAG — the C3 profile set under gpurun_out/prof_TAG/:
 #   kernel trace --stats of the default C3 bench command (single and paired screens listed as
 #   their own instantiations), then FETCH_SIZE and WRITE_SIZE passes (separate runs) over 6
 #   timed steps, whose searches include paired screens.
