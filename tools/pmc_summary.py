@@ -25,10 +25,11 @@ def main():
                 name = row["Kernel_Name"]
                 for short in KERNELS:
                     # the solver's instantiations: tanh, no H (and no Σy²); the fused pass at
-                    # 64 < nc <= 128 is the warp-specialised k_eval_fused_ws<dens, Q>
+                    # 64 < nc <= 128 is k_eval_fused_g8x<dens, Q> (digit G) or k_eval_fused_ws<dens, Q>
                     tmpl = name.split("<")[1] if "<" in name else ""
                     if short in name and (tmpl.startswith("8, ") or (short == "k_screen_oz" and "<3, 8>" in name) or
-                                          (short == "k_eval_fused" and "k_eval_fused_ws<0," in name) or
+                                          (short == "k_eval_fused" and ("k_eval_fused_ws<0," in name or
+                                                                        "k_eval_fused_g8x<0," in name)) or
                                           (short == "k_eval_loss" and ("k_eval_loss2<0, false," in name or
                                                                        "k_eval_loss_oz<0, false," in name))):
                         vals[(short, kname(name))][row["Counter_Name"]].append(float(row["Counter_Value"]))
@@ -37,7 +38,8 @@ def main():
         cands = [k for k in vals if k[0] == short and vals[k]["FETCH_SIZE"]]
         if not cands:
             continue
-        best = max(cands, key=lambda k: len(vals[k]["FETCH_SIZE"]))
+        # the default fused pass since round 5 is the digit G kernel: it wins when both ran
+        best = max(cands, key=lambda k: ("g8x" in k[1], len(vals[k]["FETCH_SIZE"])))
         v = vals[best]
         fetch = sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
         write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) if v["WRITE_SIZE"] else 0.0
