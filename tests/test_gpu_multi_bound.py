@@ -7,9 +7,10 @@ solver then rejects a try only when its lower bound cannot beat the current loss
 every acceptance on the exact loss of a full pass (core.rs:127-140 on exact values). Checked
 here: the bound covers the exact loss-only pass at every try, over W of very different
 scales, at the register-resident (nc ≤ 128) and the tiled (nc = 256) shapes; it is tight
-(≤ 1e-5 of Σℓ); and a C4-shape fit takes the same decisions with it (the default: the solver
-uses it until its first wasted full pass) as with the exact multi-try pass
-(PICARD_MULTI_F32=0): same iterations, bit-identical unmixing."""
+(≤ 1e-5 of Σℓ); and a C4-shape fit takes the same decisions with it (opt-in,
+PICARD_MULTI_F32=1: the solver then uses it until its first wasted full pass) as
+with the exact multi-try pass (the default, PICARD_MULTI_F32=0): same iterations, bit-identical
+unmixing."""
 import numpy as np
 import pytest
 
