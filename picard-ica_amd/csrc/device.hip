@@ -879,7 +879,6 @@ k_eval_fused(const double* __restrict__ X, uint64_t ldx, uint64_t n_local, int n
 #include "fused_ws.inc"
 #include "fused_g8.inc"   // G = ψ·Yᵀ on int8 digits: the arithmetic
 #include "fused_g8x.inc"  // … and the kernel (8 waves, G interleaved with the Y stage)
-#include "fused_g8y.inc"  // the same with one wave per SIMD, MFMAs paired with vector work (opt-in)
 
 // ---------------------------------------------------------------------------
 // Split evaluation for line-search tries (bit-identical sums to k_eval_fused):
@@ -3007,16 +3006,10 @@ struct DeviceCtx : Evaluator {
           const double bound = 1.0 / std::sqrt(alpha * 2.718281828459045) * (1.0 + 1e-12);
           psc = std::ldexp(1.0, 46 - (std::ilogb(bound) + 1));
         }
+        auto kg8x = k_eval_fused_g8x<D, Q>;
+        lds_attr((const void*)kg8x, G8X_LDS);
         HIP_OK(hipEventRecord(ev[1], stream));
-        if (g8y_) {
-          auto kg8y = k_eval_fused_g8y<D, Q>;
-          lds_attr((const void*)kg8y, G8Y_LDS);
-          kg8y<<<nwg, G8Y_THREADS, G8Y_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
-        } else {
-          auto kg8x = k_eval_fused_g8x<D, Q>;
-          lds_attr((const void*)kg8x, G8X_LDS);
-          kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
-        }
+        kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
         HIP_OK(hipGetLastError());
         ++n_int8_passes_;
         ++n_g8_passes_;
@@ -3595,8 +3588,6 @@ struct DeviceCtx : Evaluator {
   // d_wsc[256 …] are valid for the W image and the digit image whose largest sample exponent is
   // g8_emax_
   int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) == 0) ? 1 : 0;
-  // PICARD_G8Y=1: the digit G stage as k_eval_fused_g8y (one wave per SIMD; same bits)
-  const bool g8y_ = std::getenv("PICARD_G8Y") && std::atoi(std::getenv("PICARD_G8Y")) == 1;
   bool g8_scales_ok_ = false;
 
   int g8_emax_ = INT_MIN;
