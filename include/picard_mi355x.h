@@ -385,6 +385,11 @@ enum { PC_GSTAGE_AUTO = 0, PC_GSTAGE_F64 = 1 };
 int pc_ctx_set_g_stage(pc_ctx* ctx, int32_t mode);
 /* number of fused passes whose G stage ran on int8 digits since the context was created */
 uint64_t pc_ctx_g8_passes(const pc_ctx* ctx);
+/* number of non-ortho multi-try passes (pc_ctx_eval_loss_multi, core.rs:117-141) that read Y
+ * from the tiled full pass at the same W instead of forming it (the same bits: both come from
+ * the same int8 digit products; PICARD_MULTI_YBUF=0 in the environment turns this off for new
+ * contexts) */
+uint64_t pc_ctx_multi_ybuf_passes(const pc_ctx* ctx);
 /* The line-search screen itself: ll_out[i] = Σℓ of row i from the 4 leading digit
  * diagonals, bound_out[i] ≥ |Σℓ_exact − ll_out[i]| (rounding included), both summed
  * over ranks. Returns PC_ERR_UNSUPPORTED when the context has no screen for this

@@ -41,6 +41,7 @@ void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int rese
 void device_ctx_set_y_stage(Evaluator* e, int mode);
 void device_ctx_set_g_stage(Evaluator* e, int mode);
 uint64_t device_ctx_g8_passes(const Evaluator* e);
+uint64_t device_ctx_multi_ybuf_passes(const Evaluator* e);
 uint64_t device_ctx_int8_passes(const Evaluator* e);
 void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset);
 uint64_t device_ctx_screen_tries(const Evaluator* e);
@@ -510,6 +511,7 @@ int pc_ctx_set_g_stage(pc_ctx* c, int32_t mode) {
 }
 
 uint64_t pc_ctx_g8_passes(const pc_ctx* c) { return device_ctx_g8_passes(c->ev.get()); }
+uint64_t pc_ctx_multi_ybuf_passes(const pc_ctx* c) { return device_ctx_multi_ybuf_passes(c->ev.get()); }
 
 int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density density,
                             double* ll_out, double* bound_out, char* err, size_t errlen) {

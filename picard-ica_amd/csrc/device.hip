@@ -1985,6 +1985,114 @@ k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc
   }
 }
 
+// k_multi_loss2_oz with Y read back instead of formed: the tiled full pass at the same W
+// (k_tiled_yw_oz MODE 0, one T chunk) left Y in HBM in fragment order, from the same digit
+// products, scales and combine, so the same bits (core.rs:124 keeps Y between passes too). Each
+// wave forms only the Zᵀ tile of its row block 8·role + w (image row blocks 16–31) and evaluates
+// every try on y = Y + α_j·Z: half the matrix work per try of k_multi_loss2_oz, no exchange. The
+// host passes k_multi_loss2_oz's sample partition (nwgx, bpw), and each lane sums its samples
+// in that kernel's order, so the per-workgroup partials — and every decision — are bit for bit
+// the same. NT = the tries' accumulators held (10: ls_tries = 10 fits without spilling at KSO = 4).
+template <int KSO, int DENS, bool NEED_Q, int NT>
+__global__ void __launch_bounds__(FUSED_THREADS, 1)
+k_multi_loss2_ozy(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc, const uint8_t* __restrict__ wsl_g,
+                  const double* __restrict__ wsc, int ncp, double alpha, const double* __restrict__ alphas, int na,
+                  const double* __restrict__ ybuf, uint64_t bpw, uint64_t n_blocks, double* __restrict__ partials,
+                  uint64_t nwgx) {
+  constexpr int TILE = oz_block_bytes<KSO>(), NITEM = OZ_SLICES * KSO + 1, NU = (NITEM + 7) / 8;
+  constexpr int SLOT = TILE + 256, KSW = KSO < 2 ? 2 : KSO;
+  static_assert(NT <= ML_NA, "tries per pass");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nib = ncp / 16;
+  uint64_t wx;
+  int role;
+  if (!xcd_decode((nib + 7) / 8, nwgx, wx, role)) return;
+  const int ib = role * 8 + wave;
+  const bool active = ib < nib;
+  const int row = ib * 16 + lr;
+  const double inv_alpha = 1.0 / alpha, m2a = -2.0 * alpha;
+  extern __shared__ double smem[];
+  EXP_TAB_DECL;
+  exp_tab_load(s_exp_tab);
+  uint8_t* xs0 = (uint8_t*)smem;  // [2][SLOT]
+  v4i wsl[OZ_SLICES][KSO];
+#pragma unroll
+  for (int a = 0; a < OZ_SLICES; ++a)
+#pragma unroll
+    for (int k = 0; k < KSO; ++k)
+      wsl[a][k] = active ? *(const v4i*)(wsl_g + (size_t)((((16 + ib) * OZ_SLICES + a) * KSW + k) * 64 + lane) * 16)
+                         : v4i{0, 0, 0, 0};
+  const double rsc = active ? wsc[256 + row] : 0.0;
+  RowAcc racc[NT];
+  const uint64_t b_begin = wx * bpw;
+  const uint64_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  auto stage = [&](uint64_t b, uint8_t* xs) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int it = wave + 8 * u;
+      if (it < NITEM - 1)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(xsl + b * TILE + it * 1024 + lane * 16),
+                                         (lds_vptr)(xs + it * 1024), 16, 0, 0);
+      else if (it == NITEM - 1)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)((const uint32_t*)(xsc + b * 16) + (lane & 31)),
+                                         (lds_vptr)(xs + TILE), 4, 0, 0);
+    }
+  };
+  auto yload = [&](uint64_t b) {
+    d4 v;
+    const size_t f0 = tl_frag(b >> 2, ib, (int)(b & 3), 0, nib) + lane;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = ybuf[f0 + 64 * r];
+    return v;
+  };
+  if (b_begin < b_end) {
+    stage(b_begin, xs0);
+    __syncthreads();
+    int cur = 0;
+    for (uint64_t b = b_begin; b < b_end; ++b) {
+      // Y before the DMA, so that waiting for Y leaves the DMA in flight (in-order counter)
+      const d4 yv = active ? yload(b) : d4{0, 0, 0, 0};
+      if (b + 1 < b_end) stage(b + 1, xs0 + (cur ^ 1) * SLOT);
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) {
+        const uint8_t* tile = xs0 + cur * SLOT;
+        v4i acc[OZ_SLICES];
+        oz_ystage<OZ_SLICES - 1, KSO>(tile, lane, wsl, acc);
+        const double* scd = (const double*)(tile + TILE);
+        const double x4[4] = {scd[lk], scd[lk + 4], scd[lk + 8], scd[lk + 12]};
+        const d4 zv = oz_combine(acc, rsc, x4);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          if (u < na) {
+            const double aj = alphas[u];
+            d4 yj;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj, zv[r], yv[r]);
+            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, s_exp_tab, racc[u]);
+            if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
+          }
+        }
+      }
+      dma_barrier<0>();  // this wave's LDS-DMA of block b + 1 landed
+      cur ^= 1;
+    }
+  }
+  double* out = partials + (size_t)wx * ML_NA * 2 * ncp;
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    if (u < na) {
+      double l = acc_ll<DENS>(racc[u], inv_alpha, b_begin < b_end ? 4 * (int)(b_end - b_begin) : 0), q = racc[u].q;
+      l += __shfl_xor(l, 16); l += __shfl_xor(l, 32);
+      q += __shfl_xor(q, 16); q += __shfl_xor(q, 32);
+      if (active && lk == 0) {
+        out[(u * 2 + 0) * ncp + row] = l;
+        out[(u * 2 + 1) * ncp + row] = q;
+      }
+    }
+  }
+}
+
 // stats[e] for the tiled path: G/H from slabs (sum over splits), rows from phase-1 partials.
 // Row terms from k_tiled_yw are raw (finalize_row with dens ≥ 0); k_tiled_y's are final (dens < 0).
 __global__ void k_reduce_tiled(const double* __restrict__ slabs, int nsplit, const double* __restrict__ rows,
@@ -3166,6 +3274,27 @@ struct DeviceCtx : Evaluator {
       default: multi2_oz_launch<4, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part, f32); break;
     }
   }
+  // k_multi_loss2_ozy on k_multi_loss2_oz's partition (nwg, bpw): the same partials
+  template <int KSO, int D>
+  void multi2_ozy_launch(int ncp, double alpha, const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks,
+                         double* part) {
+    const int nroles = (ncp / 16 + 7) / 8;
+    const size_t lds = (size_t)2 * (oz_block_bytes<KSO>() + 256);
+    auto k = na <= 10 ? (want_y2 ? k_multi_loss2_ozy<KSO, D, true, 10> : k_multi_loss2_ozy<KSO, D, false, 10>)
+                      : (want_y2 ? k_multi_loss2_ozy<KSO, D, true, ML_NA> : k_multi_loss2_ozy<KSO, D, false, ML_NA>);
+    lds_attr((const void*)k, (int)lds);
+    k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, ncp, alpha, dal, na, d_tbuf,
+                                                             bpw, n_blocks, part, (uint64_t)nwg);
+  }
+  template <int D>
+  void multi2_ozy_dispatch(int ncp, double alpha, const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks,
+                           double* part) {
+    switch (oz_kso()) {
+      case 1: multi2_ozy_launch<1, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      case 2: multi2_ozy_launch<2, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+      default: multi2_ozy_launch<4, D>(ncp, alpha, dal, na, nwg, bpw, n_blocks, part); break;
+    }
+  }
   template <int D>
   void multi2_dispatch(int ks, int ncp, const double* dw, const double* dz, const double* dmu, double alpha,
                        const double* dal, int na, int nwg, uint64_t bpw, uint64_t n_blocks, double* part) {
@@ -3207,8 +3336,22 @@ struct DeviceCtx : Evaluator {
       bool oz = y_stage_ != 1 && dmu == nullptr && ensure_xsl();
       if (oz) upload_wsl2(w, z, nc);
       oz = oz && xsl_valid_;
+      // Y of this W already in HBM (the full tiled pass before this search): read, not formed
+      // (tanh at 256 features holds its tries' accumulators without spilling only without Σy² and
+      // with ≤ 10 tries: otherwise k_multi_loss2_oz)
+      const bool ozy_fits = !(oz_kso() == 4 && d.kind == DENS_TANH && (want_y2 || na > 10));
+      const bool ytile = oz && multi_ybuf_ && ozy_fits && ytile_valid_ && ytile_nc_ == nc && ytile_gen_ == xsl_gen_ &&
+                         ytile_w_.size() == nc * nf && std::memcmp(ytile_w_.data(), w, nc * nf * sizeof(double)) == 0;
       HIP_OK(hipEventRecord(ev[1], stream));
-      if (oz) {
+      if (ytile) {
+        switch (d.kind) {
+          case DENS_TANH: multi2_ozy_dispatch<DENS_TANH>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+          case DENS_EXP: multi2_ozy_dispatch<DENS_EXP>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+          default: multi2_ozy_dispatch<DENS_CUBE>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
+        }
+        ++n_int8_passes_;
+        ++n_multi_ybuf_;
+      } else if (oz) {
         switch (d.kind) {
           case DENS_TANH: multi2_oz_dispatch<DENS_TANH>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
           case DENS_EXP: multi2_oz_dispatch<DENS_EXP>(ncp, d.alpha, dal, na, nwg, bpw, n_blocks, part); break;
@@ -3388,6 +3531,16 @@ struct DeviceCtx : Evaluator {
 
   // ---- tiled two-phase path ----------------------------------------------
   double* d_tbuf = nullptr; size_t cap_tbuf = 0;   // y, ψ, ψ′ fragments of one T chunk
+  // Y of the whole shard left in d_tbuf by the last full tiled pass on the int8 stage: valid
+  // for W = ytile_w_ (nc rows) and the digit image of generation ytile_gen_; the multi-try
+  // pass at that W reads it instead of forming Y again (k_multi_loss2_ozy).
+  // PICARD_MULTI_YBUF=0 (A/B knob) forms Y in every multi-try pass.
+  bool ytile_valid_ = false;
+  size_t ytile_nc_ = 0;
+  uint64_t ytile_gen_ = 0;
+  std::vector<double> ytile_w_;
+  uint64_t n_multi_ybuf_ = 0;
+  const bool multi_ybuf_ = !(std::getenv("PICARD_MULTI_YBUF") && std::atoi(std::getenv("PICARD_MULTI_YBUF")) == 0);
   double* d_slab = nullptr; size_t cap_slab = 0;
   double* d_trow = nullptr; size_t cap_trow = 0;
   double tiled_budget_ = 0;  // bytes the fragment buffers may take (set on first use)
@@ -3489,6 +3642,7 @@ struct DeviceCtx : Evaluator {
     const int ncp = (int)((nc + 31) / 32 * 32);
     const int ks = yw_ks(nf);
     const uint64_t kc = 4 * (uint64_t)ks, nfp = (nf + kc - 1) / kc * kc;
+    if (mode == 0 || nf > kc) ytile_valid_ = false;  // this pass writes the y fragments
     std::vector<double> wt((size_t)nfp * ncp, 0.0);  // Wᵀ, zero-padded to whole feature chunks
     for (size_t i = 0; i < nc; ++i)
       for (size_t k = 0; k < nf; ++k) wt[k * ncp + i] = w[i * nf + k];
@@ -3539,6 +3693,12 @@ struct DeviceCtx : Evaluator {
         default: tiled_launch<DENS_LINEAR>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, false, t0); break;
       }
     }
+    if (mode == 0 && oz && ct >= std::max<uint64_t>(n_tiles, 1)) {  // one chunk: all of Y stays
+      ytile_valid_ = true;
+      ytile_nc_ = nc;
+      ytile_gen_ = xsl_gen_;
+      ytile_w_.assign(w, w + nc * nf);
+    }
     const size_t total = (size_t)(mode == 0 ? (need_h ? 2 : 1) * nc * nc : 0) + 3 * nc;
     k_reduce_tiled<<<(total + 255) / 256, 256, 0, stream>>>(d_slab, nsplit, d_trow, nwg1, ncp, (int)nc, need_h,
                                                             mode == 1 ? 1 : 0, st, td, alpha, (double)n_local_);
@@ -3579,6 +3739,7 @@ struct DeviceCtx : Evaluator {
   double* d_xsc = nullptr;
   size_t cap_xsl = 0;
   bool xsl_valid_ = false, xsl_failed_ = false;
+  uint64_t xsl_gen_ = 0;  // digit images built so far (k_slice_x launches)
   uint8_t* d_wsl = nullptr;
   double* d_wsc = nullptr;
   int y_stage_ = 0;
@@ -3669,6 +3830,7 @@ struct DeviceCtx : Evaluator {
     else if (oz_kso() == 2) k_slice_x<2><<<grid, 128, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     else k_slice_x<4><<<grid, 256, 0, stream>>>(X, ldx, (int)nf, n_blocks, d_xsl, d_xsc);
     HIP_OK(hipGetLastError());
+    ++xsl_gen_;
     {  // Σ_t 2^e_t of this shard (padding included: it only loosens the screen's bound)
       const int nwg = nwg_e;
       const uint64_t per = ((ldx + nwg - 1) / nwg + 511) / 512 * 512;
@@ -4804,6 +4966,9 @@ void device_ctx_kernel_breakdown(Evaluator* e, double* ms, uint64_t* n, int rese
 }
 void device_ctx_set_g_stage(Evaluator* e, int mode) { static_cast<DeviceCtx*>(e)->g_stage_ = mode; }
 uint64_t device_ctx_g8_passes(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_g8_passes_; }
+uint64_t device_ctx_multi_ybuf_passes(const Evaluator* e) {
+  return static_cast<const DeviceCtx*>(e)->n_multi_ybuf_;
+}
 void device_ctx_set_y_stage(Evaluator* e, int mode) {
   auto* d = static_cast<DeviceCtx*>(e);
   d->y_stage_ = mode;
