@@ -1476,15 +1476,17 @@ k_tiled_yw_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc, c
 // DFROMP (tanh, α > 0): ψ′ = α(1 − ψ²) is formed here from the staged ψ — the
 // expression density_acc4 evaluates, so the same bits — instead of being
 // written by phase 1 and read back (one array less each way).
-template <bool NEED_H, bool DFROMP>
+template <bool NEED_H, bool DFROMP, int SBB = 2>
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
 k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, const double* __restrict__ dbuf,
               int ncp, uint64_t n_tiles, uint64_t tps, double* __restrict__ slabs, int accumulate, double alpha,
               uint64_t nsplit) {
   static_assert(NEED_H || !DFROMP, "ψ′ only feeds H");
+  static_assert(SBB == 1 || SBB == 2 || SBB == 4, "sub-blocks per stage divide a 64-sample tile");
   constexpr int NARR = NEED_H && !DFROMP ? 3 : 2;  // staged arrays: ψ, y (, ψ′)
   constexpr int SUB = 8 * 256;          // doubles per array per sub-block (8 row blocks × 4 r × 64)
   constexpr int PRE = NARR * SUB / 2 / FUSED_THREADS;  // 2 slots per array
+  constexpr int STG = SBB * NARR * SUB;  // doubles per stage (SBB sub-blocks, one barrier)
   static_assert(SUB == 4 * FUSED_THREADS, "slot map assumes 512 threads");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
@@ -1496,7 +1498,7 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
   const int ti = tile / nto, tj = tile % nto;
   const int gi0 = (wave >> 2) * 4, gj0 = (wave & 3) * 2;  // local row blocks
   extern __shared__ double smem[];
-  double* lds = smem;  // [2][NARR][8][4][64]
+  double* lds = smem;  // [2][SBB][NARR][8][4][64]
   d4 accg[4][2], acch[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1516,50 +1518,59 @@ k_tiled_gram2(const double* __restrict__ ybuf, const double* __restrict__ pbuf, 
   }
   const uint64_t t_begin = split * tps;
   const uint64_t t_end = t_begin + tps < n_tiles ? t_begin + tps : n_tiles;
-  const uint64_t s_begin = t_begin * 4, s_end = t_end * 4;  // sub-blocks
-  double2 pre[PRE];
-  auto load = [&](uint64_t sb) {
-    const size_t o = ((sb >> 2) * (size_t)nib * 4 + (sb & 3)) * 256;
+  const uint64_t s_begin = t_begin * 4, s_end = t_end * 4;  // sub-blocks (a multiple of SBB apart)
+  double2 pre[SBB][PRE];
+  auto load = [&](uint64_t sb0) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) {
-      const double* base = (p >> 1) == 0 ? pbuf : (p >> 1) == 1 ? ybuf : dbuf;
-      pre[p] = ok[p] ? *reinterpret_cast<const double2*>(base + o + soff[p]) : double2{0.0, 0.0};
+    for (int q = 0; q < SBB; ++q) {
+      const uint64_t sb = sb0 + q;
+      const size_t o = ((sb >> 2) * (size_t)nib * 4 + (sb & 3)) * 256;
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        const double* base = (p >> 1) == 0 ? pbuf : (p >> 1) == 1 ? ybuf : dbuf;
+        pre[q][p] = ok[p] ? *reinterpret_cast<const double2*>(base + o + soff[p]) : double2{0.0, 0.0};
+      }
     }
   };
   auto store = [&](double* img) {
 #pragma unroll
-    for (int p = 0; p < PRE; ++p) *reinterpret_cast<double2*>(img + 2 * tid + 1024 * p) = pre[p];
+    for (int q = 0; q < SBB; ++q)
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) *reinterpret_cast<double2*>(img + q * NARR * SUB + 2 * tid + 1024 * p) = pre[q][p];
   };
   if (s_begin < s_end) {
     load(s_begin);
     store(lds);
     __syncthreads();
     int cur = 0;
-    for (uint64_t sb = s_begin; sb < s_end; ++sb) {
-      load(sb + 1 < s_end ? sb + 1 : sb);
+    for (uint64_t sb = s_begin; sb < s_end; sb += SBB) {
+      load(sb + SBB < s_end ? sb + SBB : sb);
       __builtin_amdgcn_sched_barrier(0);
-      const double* img = lds + cur * NARR * SUB;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double pa[4], da[4], yb[2];
+      for (int q = 0; q < SBB; ++q) {
+        const double* img = lds + cur * STG + q * NARR * SUB;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          pa[i] = img[((gi0 + i) * 4 + r) * 64 + lane];
-          if constexpr (DFROMP) da[i] = alpha * __builtin_fma(-pa[i], pa[i], 1.0);
-          else if constexpr (NEED_H) da[i] = img[2 * SUB + ((gi0 + i) * 4 + r) * 64 + lane];
-        }
+        for (int r = 0; r < 4; ++r) {
+          double pa[4], da[4], yb[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) yb[j] = img[SUB + ((gj0 + j) * 4 + r) * 64 + lane];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            accg[i][j] = mfma(pa[i], yb[j], accg[i][j]);
-            if constexpr (NEED_H) acch[i][j] = mfma(da[i], yb[j] * yb[j], acch[i][j]);
+          for (int i = 0; i < 4; ++i) {
+            pa[i] = img[((gi0 + i) * 4 + r) * 64 + lane];
+            if constexpr (DFROMP) da[i] = alpha * __builtin_fma(-pa[i], pa[i], 1.0);
+            else if constexpr (NEED_H) da[i] = img[2 * SUB + ((gi0 + i) * 4 + r) * 64 + lane];
           }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) yb[j] = img[SUB + ((gj0 + j) * 4 + r) * 64 + lane];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              accg[i][j] = mfma(pa[i], yb[j], accg[i][j]);
+              if constexpr (NEED_H) acch[i][j] = mfma(da[i], yb[j] * yb[j], acch[i][j]);
+            }
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
-      store(lds + (cur ^ 1) * NARR * SUB);
+      store(lds + (cur ^ 1) * STG);
       __syncthreads();
       cur ^= 1;
     }
@@ -3311,19 +3322,28 @@ struct DeviceCtx : Evaluator {
     const int ncp = (int)((nc + 31) / 32 * 32);
     const int ks = yw_ks(nf);  // nf ≤ 256: register-resident k_multi_loss2
     const int nfp = ks ? 4 * ks : (int)((nf + ML_KC - 1) / ML_KC * ML_KC);
-    std::vector<double> wt((size_t)2 * nfp * ncp + ML_NA, 0.0);
-    for (size_t i = 0; i < nc; ++i)
-      for (size_t k = 0; k < nf; ++k) {
-        wt[k * ncp + i] = w[i * nf + k];
-        wt[(size_t)nfp * ncp + k * ncp + i] = z[i * nf + k];
-      }
-    for (int j = 0; j < na; ++j) wt[(size_t)2 * nfp * ncp + j] = alphas[j];
-    double* dw = ensure(d_w, cap_w, wt.size());
+    const size_t nwt = (size_t)2 * nfp * ncp + ML_NA;
+    double* dw = ensure(d_w, cap_w, nwt);
     HIP_OK(hipEventRecord(ev[0], stream));
-    HIP_OK(hipMemcpyAsync(dw, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    // [Wᵀ | Zᵀ | α] for the fp64 kernels; the int8 kernels take W and Z from their digit images
+    // and only need the α's
+    auto upload_wt = [&](bool full) {
+      std::vector<double> wt(full ? nwt : (size_t)ML_NA, 0.0);
+      double* al = wt.data() + (full ? (size_t)2 * nfp * ncp : 0);
+      if (full)
+        for (size_t i = 0; i < nc; ++i)
+          for (size_t k = 0; k < nf; ++k) {
+            wt[k * ncp + i] = w[i * nf + k];
+            wt[(size_t)nfp * ncp + k * ncp + i] = z[i * nf + k];
+          }
+      for (int j = 0; j < na; ++j) al[j] = alphas[j];
+      HIP_OK(hipMemcpyAsync(full ? dw : dw + (size_t)2 * nfp * ncp, wt.data(), wt.size() * sizeof(double),
+                            hipMemcpyHostToDevice, stream));
+    };
     const double* dmu = resident_mu(mu);  // null: X is centred in place
     const size_t pst = (size_t)ML_NA * 2 * ncp;
     const double* dal = dw + (size_t)2 * nfp * ncp;
+    if (!ks) upload_wt(true);
     if (ks) {
       const uint64_t n_blocks = std::max<uint64_t>((n_local_ + 15) / 16, 1);
       const int nroles = (ncp / 16 + 3) / 4;
@@ -3342,6 +3362,7 @@ struct DeviceCtx : Evaluator {
       const bool ozy_fits = !(oz_kso() == 4 && d.kind == DENS_TANH && (want_y2 || na > 10));
       const bool ytile = oz && multi_ybuf_ && ozy_fits && ytile_valid_ && ytile_nc_ == nc && ytile_gen_ == xsl_gen_ &&
                          ytile_w_.size() == nc * nf && std::memcmp(ytile_w_.data(), w, nc * nf * sizeof(double)) == 0;
+      upload_wt(!oz);
       HIP_OK(hipEventRecord(ev[1], stream));
       if (ytile) {
         switch (d.kind) {
@@ -3398,6 +3419,7 @@ struct DeviceCtx : Evaluator {
     allreduce(st, (size_t)2 * na * nc, "loss_multi");
     std::vector<double> h((size_t)2 * na * nc);
     const double* staged = d2h_enqueue(st, h.size());
+    run_overlap();  // the caller's host work while the pass runs
     finish_timing(true, 3);
     copy_out(h.data(), staged, h.size());
     for (int j = 0; j < na; ++j) {
@@ -3541,6 +3563,7 @@ struct DeviceCtx : Evaluator {
   std::vector<double> ytile_w_;
   uint64_t n_multi_ybuf_ = 0;
   const bool multi_ybuf_ = !(std::getenv("PICARD_MULTI_YBUF") && std::atoi(std::getenv("PICARD_MULTI_YBUF")) == 0);
+  const int gram_sbb_ = std::getenv("PICARD_GRAM_SBB") && std::atoi(std::getenv("PICARD_GRAM_SBB")) == 1 ? 1 : 2;
   double* d_slab = nullptr; size_t cap_slab = 0;
   double* d_trow = nullptr; size_t cap_trow = 0;
   double tiled_budget_ = 0;  // bytes the fragment buffers may take (set on first use)
@@ -3628,10 +3651,15 @@ struct DeviceCtx : Evaluator {
       const int nto = (ncp / 16 + 7) / 8;
       const uint64_t tps = (ntl + nsplit - 1) / nsplit;
       const size_t lds2 = (size_t)2 * (db ? 3 : 2) * 8 * 256 * sizeof(double);
-      auto k2 = !need_h ? k_tiled_gram2<false, false> : dfromp ? k_tiled_gram2<true, true> : k_tiled_gram2<true, false>;
+      // two sub-blocks per barrier (PICARD_GRAM_SBB=1: one) where both buffers fit the LDS
+      const int sbb = gram_sbb_ == 1 || (size_t)2 * lds2 > 160 * 1024 ? 1 : 2;
+      auto k2 = sbb == 1 ? (!need_h ? k_tiled_gram2<false, false, 1>
+                            : dfromp ? k_tiled_gram2<true, true, 1> : k_tiled_gram2<true, false, 1>)
+                         : (!need_h ? k_tiled_gram2<false, false, 2>
+                            : dfromp ? k_tiled_gram2<true, true, 2> : k_tiled_gram2<true, false, 2>);
       lds_attr((const void*)k2, 160 * 1024);
-      k2<<<xcd_grid(nsplit, nto * nto), FUSED_THREADS, lds2, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab, acc ? 1 : 0,
-                                                                       alpha, (uint64_t)nsplit);
+      k2<<<xcd_grid(nsplit, nto * nto), FUSED_THREADS, lds2 * sbb, stream>>>(yb, pb, db, ncp, ntl, tps, d_slab,
+                                                                             acc ? 1 : 0, alpha, (uint64_t)nsplit);
       HIP_OK(hipGetLastError());
     }
   }
@@ -3643,11 +3671,7 @@ struct DeviceCtx : Evaluator {
     const int ks = yw_ks(nf);
     const uint64_t kc = 4 * (uint64_t)ks, nfp = (nf + kc - 1) / kc * kc;
     if (mode == 0 || nf > kc) ytile_valid_ = false;  // this pass writes the y fragments
-    std::vector<double> wt((size_t)nfp * ncp, 0.0);  // Wᵀ, zero-padded to whole feature chunks
-    for (size_t i = 0; i < nc; ++i)
-      for (size_t k = 0; k < nf; ++k) wt[k * ncp + i] = w[i * nf + k];
-    ensure(d_w, cap_w, wt.size());
-    HIP_OK(hipMemcpyAsync(d_w, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    ensure(d_w, cap_w, (size_t)nfp * ncp);  // Wᵀ for the fp64 phase 1 (uploaded below)
     const uint64_t n_tiles = (n_local_ + TL_TT - 1) / TL_TT;
     // T chunks bound the fragment buffers (3 arrays of ncp × chunk) by what HBM
     // has free next to X (at least 24 GB): C4 (256 × 1e7, 61 GB) is one chunk
@@ -3680,6 +3704,12 @@ struct DeviceCtx : Evaluator {
     bool oz = y_stage_ != 1 && nf <= 256 && td != DENS_LINEAR && ensure_xsl();
     if (oz) upload_wsl(w, nc);
     oz = oz && xsl_valid_;
+    if (!oz) {  // Wᵀ, zero-padded to whole feature chunks (the int8 phase 1 reads W's digit image)
+      std::vector<double> wt((size_t)nfp * ncp, 0.0);
+      for (size_t i = 0; i < nc; ++i)
+        for (size_t k = 0; k < nf; ++k) wt[k * ncp + i] = w[i * nf + k];
+      HIP_OK(hipMemcpyAsync(d_w, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+    }
     for (uint64_t t0 = 0; t0 < std::max<uint64_t>(n_tiles, 1); t0 += ct) {
       const uint64_t ntl = std::min<uint64_t>(ct, std::max<uint64_t>(n_tiles, 1) - t0);
       const bool acc = t0 > 0;

@@ -4,6 +4,7 @@
 // is one of these calls; everything else is N×N host work.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -60,6 +61,17 @@ class Evaluator {
   // want_y2 (the orthogonal solver never reads it: core.rs:221 computes Y∘Y
   // but only :274 and the extended non-orthogonal loss use it). Otherwise 0.
   bool want_y2 = true;
+  // Host work the caller overlaps with its next pass (the non-ortho search's per-try W_j and
+  // log|det W_j|): an evaluator that can calls run_overlap() once the pass is enqueued and before
+  // it waits for it; the caller runs whatever is still pending after the call itself.
+  std::function<void()> overlap_;
+  void run_overlap() {
+    if (overlap_) {
+      auto f = std::move(overlap_);
+      overlap_ = nullptr;
+      f();
+    }
+  }
   virtual uint64_t n_features() const = 0;
   virtual uint64_t n_samples() const = 0;  // global T over all ranks
   // true for a detached shard (world > 1, no communicator): every statistic is

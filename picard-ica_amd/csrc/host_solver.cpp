@@ -268,6 +268,10 @@ void Solver::evaluate(const Mat& w_core, EvalStats* out) {
   eval_ms_ += now_ms() - t0;
   ++last_evals_;
   ++total_evals_;
+  if (!cfg_.ortho) {  // the next non-ortho search starts from this W: keep W·P for it
+    wp_cache_src_ = w_core;
+    wp_cache_ = std::move(wt);
+  }
 }
 
 bool Solver::evaluate_loss(const Mat& w_core, EvalStats* out) {
@@ -565,7 +569,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       } else {
         r.w = ahead_->get(k, &ahead_wait_ms_);
       }
-    } else {
+    } else if (no_multi_ || !(k == 1 || (k == 0 && multi_first))) {  // (a multi-try pass forms it below)
       transform = Mat::eye(n);
       for (size_t e = 0; e < transform.a.size(); ++e) transform.a[e] += alpha * direction.a[e];
       r.w = matmul(transform, W_);
@@ -576,7 +580,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       const size_t na = tries - k;
       std::vector<double> alphas(na), ll(na * n), y2(na * n), bnd;
       for (size_t j = 0; j < na; ++j) alphas[j] = j == 0 ? alpha : alphas[j - 1] / 2.0;
-      Mat wt = matmul(W_, P_);
+      const bool cached = wp_cache_src_.a.size() == W_.a.size() &&
+                          std::memcmp(wp_cache_src_.a.data(), W_.a.data(), W_.a.size() * sizeof(double)) == 0;
+      const Mat wt = cached ? wp_cache_ : matmul(W_, P_);  // (the same product, evaluate())
       Mat zt = matmul(matmul(direction, W_), P_);
       // without Σy² in the loss (not extended), the tries may come with a bound instead of
       // exact sums (fp32 row terms); every decision is then taken on exact values (below)
@@ -595,34 +601,42 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       // is the one-pass schedule's.
       const size_t g1 = bounded || multi_group_ == 0 ? na : std::min(na, multi_group_);
       size_t j0 = 0, nj = g1;
+      // every try's W_j = (I + α_j D)·W and log|det W_j| (core.rs:121-125, :43-47), formed for a
+      // pass's tries at once on the host threads — while the device runs that pass (the
+      // evaluator's overlap hook), else right after it; each is the same serial arithmetic as
+      // the per-try path, and the walk below accepts in the reference order
+      std::vector<Mat> wj(na);
+      std::vector<double> dsg(na), dla(na);
+      auto form_tries = [&](size_t a0, size_t cnt) {
+#pragma omp parallel for schedule(dynamic, 1) if (cnt > 1)
+        for (size_t j = a0; j < a0 + cnt; ++j) {
+          Mat tj = Mat::eye(n);
+          for (size_t e = 0; e < tj.a.size(); ++e) tj.a[e] += alphas[j] * direction.a[e];
+          wj[j] = matmul(tj, W_);
+          sln_det(wj[j], &dsg[j], &dla[j]);
+        }
+      };
+      struct HookGuard {  // never leave a hook on the evaluator that refers to this frame
+        Evaluator* ev;
+        ~HookGuard() { ev->overlap_ = nullptr; }
+      } hook_guard{ev_};
+      if (bounded) form_tries(0, nj);
+      else ev_->overlap_ = [&, nj] { form_tries(0, nj); };
       const bool multi_ran = bounded || ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr,
                                                              cfg_.density, alphas.data(), (int)nj, ll.data(), y2.data());
       eval_ms_ += now_ms() - tmp0;  // the multi-try pass is device time
+      ev_->run_overlap();  // (not run by the evaluator)
+      if (!multi_ran) r.w = wj[0];  // try k on its own pass (below)
       if (multi_ran) {
         EvalStats ls;
         ls.nc = n;
         ls.has_h = false;
         ls.buf.assign(EvalStats::size(n, false), 0.0);
-        std::vector<Mat> wj(na);
-        std::vector<double> dsg(na), dla(na);
-        wj[0] = r.w;
         EvalStats last_full;  // bounded: the exact pass of the LAST try, if one ran and rejected it
         bool have_last_full = false;
         for (;;) {  // one pass over tries j0 … j0 + nj − 1
           ++last_evals_;
           ++total_evals_;
-          // every try's W_j = (I + α_j D)·W and log|det W_j| (core.rs:124-125, :43-47),
-          // formed for the pass's tries at once on the host threads; each is the same serial
-          // arithmetic as in the walk below, which then accepts in the reference order
-#pragma omp parallel for schedule(dynamic, 1) if (nj > 1)
-          for (size_t j = j0; j < j0 + nj; ++j) {
-            if (j > 0) {
-              Mat tj = Mat::eye(n);
-              for (size_t e = 0; e < tj.a.size(); ++e) tj.a[e] += alphas[j] * direction.a[e];
-              wj[j] = matmul(tj, W_);
-            }
-            sln_det(wj[j], &dsg[j], &dla[j]);
-          }
           for (size_t j = j0; j < j0 + nj; ++j) {
             const double a = alphas[j];
             r.w = std::move(wj[j]);
@@ -658,7 +672,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
             } else if (loss < current_loss_) {
               evaluate(r.w, &r.stats);  // the new iterate: full pass at W_k
               r.partial = false;
-              r.loss = loss_of(r.stats, r.w, signs_, &singular);
+              r.loss = loss_of(r.stats, r.w, signs_, &singular, dsg[j], dla[j]);  // (its log|det| is formed)
               r.success = true;
               r.step = scale(direction, a);
               return r;
@@ -670,10 +684,12 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           nj = na - j0;  // the remaining tries in one more pass
           ++multi_second_passes_;
           const double tmp1 = now_ms();
+          ev_->overlap_ = [&, j0, nj] { form_tries(j0, nj); };
           if (!ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
                                     alphas.data() + j0, (int)nj, ll.data() + j0 * n, y2.data() + j0 * n))
             throw computation_error("multi-try pass refused after an earlier one ran");
           eval_ms_ += now_ms() - tmp1;
+          ev_->run_overlap();
         }
         // no try accepted: the caller evaluates the last try in full if it keeps it — unless
         // the bounded path already ran that pass (its exact statistics and loss are kept)
@@ -685,7 +701,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         } else {
           r.stats = ls;
           r.needs_full = true;
-          r.loss = loss_of(ls, r.w, signs_, &singular);
+          r.loss = loss_of(ls, r.w, signs_, &singular, dsg[na - 1], dla[na - 1]);
+          r.det_sg = dsg[na - 1];  // step() evaluates this W in full and takes its loss again
+          r.det_la = dla[na - 1];
         }
         r.partial = false;
         r.step = scale(direction, alpha);
@@ -1002,7 +1020,7 @@ bool Solver::step() {
   if (res.needs_full || res.screened_out) {  // rejected multi-try / screened last try kept as the iterate
     evaluate(res.w, &res.stats);
     bool singular;
-    res.loss = loss_of(res.stats, res.w, signs_, &singular);
+    res.loss = loss_of(res.stats, res.w, signs_, &singular, res.det_sg, res.det_la);
   }
   {
     const double step_ms = now_ms() - step_t0, dev_ms = eval_ms_ - eval_t0;

@@ -75,8 +75,9 @@ class Solver {
   bool evaluate_loss(const Mat& w_core, EvalStats* out);  // true: only Σℓ/Σy² filled, Y kept on device
   void complete(EvalStats* out);
   // screened_out: the last try was rejected by the screen alone (no exact stats for w)
+  // det_sg / det_la: sign and log|det w| when the search already formed them (NaN: not formed)
   struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full;
-                    bool screened_out; };
+                    bool screened_out; double det_sg = std::numeric_limits<double>::quiet_NaN(), det_la = 0.0; };
   LsResult line_search(const Mat& direction, size_t tries, bool multi_first, bool first_loss_only,
                        bool full_first = false);
   void init_core();
@@ -85,6 +86,7 @@ class Solver {
 
   Evaluator* ev_;
   pc_config cfg_;
+  Mat wp_cache_, wp_cache_src_;  // W·P of the last full pass and its W (non-ortho)
   std::vector<double> w_init_user_;
   uint64_t nf_ = 0, T_ = 0;
   size_t nc_ = 0;
