@@ -2761,7 +2761,7 @@ struct DeviceCtx : Evaluator {
     ctx_count_add(device, -1);
     (void)hipSetDevice(device);
     coll_.reset();
-    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src, d_jade})
+    for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_ybuf2, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src, d_jade})
       if (p) (void)t_free(p);
     for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc, (void*)d_xsf})  // d_wsl lies inside d_wsc's allocation
       if (p) (void)t_free(p);
@@ -3294,7 +3294,7 @@ struct DeviceCtx : Evaluator {
     auto k = na <= 10 ? (want_y2 ? k_multi_loss2_ozy<KSO, D, true, 10> : k_multi_loss2_ozy<KSO, D, false, 10>)
                       : (want_y2 ? k_multi_loss2_ozy<KSO, D, true, ML_NA> : k_multi_loss2_ozy<KSO, D, false, ML_NA>);
     lds_attr((const void*)k, (int)lds);
-    k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, ncp, alpha, dal, na, d_tbuf,
+    k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, ncp, alpha, dal, na, ybuf_read_,
                                                              bpw, n_blocks, part, (uint64_t)nwg);
   }
   template <int D>
@@ -3360,8 +3360,9 @@ struct DeviceCtx : Evaluator {
       // (tanh at 256 features holds its tries' accumulators without spilling only without Σy² and
       // with ≤ 10 tries: otherwise k_multi_loss2_oz)
       const bool ozy_fits = !(oz_kso() == 4 && d.kind == DENS_TANH && (want_y2 || na > 10));
-      const bool ytile = oz && multi_ybuf_ && ozy_fits && ytile_valid_ && ytile_nc_ == nc && ytile_gen_ == xsl_gen_ &&
-                         ytile_w_.size() == nc * nf && std::memcmp(ytile_w_.data(), w, nc * nf * sizeof(double)) == 0;
+      const int yslot = !(oz && multi_ybuf_ && ozy_fits) ? -1 : ytile_match(0, w, nc) ? 0 : ytile_match(1, w, nc) ? 1 : -1;
+      const bool ytile = yslot >= 0;
+      ybuf_read_ = yslot == 1 ? d_ybuf2 : d_tbuf;
       upload_wt(!oz);
       HIP_OK(hipEventRecord(ev[1], stream));
       if (ytile) {
@@ -3553,15 +3554,54 @@ struct DeviceCtx : Evaluator {
 
   // ---- tiled two-phase path ----------------------------------------------
   double* d_tbuf = nullptr; size_t cap_tbuf = 0;   // y, ψ, ψ′ fragments of one T chunk
-  // Y of the whole shard left in d_tbuf by the last full tiled pass on the int8 stage: valid
-  // for W = ytile_w_ (nc rows) and the digit image of generation ytile_gen_; the multi-try
-  // pass at that W reads it instead of forming Y again (k_multi_loss2_ozy).
+  // Y of the whole shard left in HBM by a full tiled pass on the int8 stage (one T chunk): valid
+  // for W = YTile::w (nc rows) and the digit image of generation YTile::gen; the multi-try pass
+  // at that W reads it instead of forming Y again (k_multi_loss2_ozy).
   // PICARD_MULTI_YBUF=0 (A/B knob) forms Y in every multi-try pass.
-  bool ytile_valid_ = false;
-  size_t ytile_nc_ = 0;
-  uint64_t ytile_gen_ = 0;
-  std::vector<double> ytile_w_;
+  // Two slots: slot 0 is the y region of d_tbuf, slot 1 a second buffer (d_ybuf2, allocated when
+  // HBM has room) — a full pass at a new W writes the slot the last one did not, so the W of a
+  // search keeps its Y through a rejected try-1 full pass at another W.
+  struct YTile {
+    bool valid = false;
+    size_t nc = 0;
+    uint64_t gen = 0;
+    std::vector<double> w;
+  };
+  YTile ytile_[2];
+  int ytile_last_ = 0;          // the slot the last full tiled pass wrote
+  double* ytarget_ = nullptr;   // where the current tiled pass writes its y fragments
+  double* d_ybuf2 = nullptr;
+  size_t cap_ybuf2 = 0;
+  bool ybuf2_failed_ = false;
+  bool ytile_match(int s, const double* w, size_t nc) const {
+    const YTile& y = ytile_[s];
+    return y.valid && y.nc == nc && y.gen == xsl_gen_ && y.w.size() == nc * nf &&
+           std::memcmp(y.w.data(), w, nc * nf * sizeof(double)) == 0;
+  }
+  // the second y buffer: only with ≥ 16 GB left beside it, and never at the digit image's expense
+  bool ensure_ybuf2(size_t n) {
+    if (n <= cap_ybuf2) return true;
+    if (ybuf2_failed_) return false;
+    size_t fr = 0, tot = 0;
+    HIP_OK(t_meminfo(&fr, &tot));
+    if (d_ybuf2) {
+      HIP_OK(t_free(d_ybuf2));
+      fr += cap_ybuf2 * sizeof(double);
+      d_ybuf2 = nullptr;
+      cap_ybuf2 = 0;
+      ytile_[1].valid = false;
+    }
+    if (n * sizeof(double) + (size_t(16) << 30) > fr || t_malloc((void**)&d_ybuf2, n * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      d_ybuf2 = nullptr;
+      ybuf2_failed_ = true;
+      return false;
+    }
+    cap_ybuf2 = n;
+    return true;
+  }
   uint64_t n_multi_ybuf_ = 0;
+  const double* ybuf_read_ = nullptr;  // the slot the current multi-try pass reads
   const bool multi_ybuf_ = !(std::getenv("PICARD_MULTI_YBUF") && std::atoi(std::getenv("PICARD_MULTI_YBUF")) == 0);
   const int gram_sbb_ = std::getenv("PICARD_GRAM_SBB") && std::atoi(std::getenv("PICARD_GRAM_SBB")) == 1 ? 1 : 2;
   double* d_slab = nullptr; size_t cap_slab = 0;
@@ -3628,7 +3668,7 @@ struct DeviceCtx : Evaluator {
                     const double* X0, bool oz, uint64_t t0) {
     const size_t chunk = (size_t)ncp * ntl * TL_TT;
     constexpr bool dfromp = D == DENS_TANH;  // ψ′ = α(1 − ψ²) formed in phase 2
-    double* yb = d_tbuf;
+    double* yb = ytarget_ ? ytarget_ : d_tbuf;
     double* pb = d_tbuf + chunk;
     double* db = need_h && !dfromp ? d_tbuf + 2 * chunk : nullptr;
     const uint64_t kc = 4 * (uint64_t)ks;  // features per chunk
@@ -3670,7 +3710,6 @@ struct DeviceCtx : Evaluator {
     const int ncp = (int)((nc + 31) / 32 * 32);
     const int ks = yw_ks(nf);
     const uint64_t kc = 4 * (uint64_t)ks, nfp = (nf + kc - 1) / kc * kc;
-    if (mode == 0 || nf > kc) ytile_valid_ = false;  // this pass writes the y fragments
     ensure(d_w, cap_w, (size_t)nfp * ncp);  // Wᵀ for the fp64 phase 1 (uploaded below)
     const uint64_t n_tiles = (n_local_ + TL_TT - 1) / TL_TT;
     // T chunks bound the fragment buffers (3 arrays of ncp × chunk) by what HBM
@@ -3694,8 +3733,10 @@ struct DeviceCtx : Evaluator {
     const int nto = (ncp / 16 + 7) / 8;
     const int nsplit = (int)std::max<uint64_t>(1, std::min<uint64_t>(ct, (uint64_t)(2 * n_cu / (nto * nto))));
     // y buffer: always in mode 0; in mode 1 only to carry partial y across feature chunks
+    const double* tbuf0 = d_tbuf;
     if (mode == 0) ensure(d_tbuf, cap_tbuf, (size_t)narr * ncp * ct * TL_TT);
     else if (nf > kc) ensure(d_tbuf, cap_tbuf, (size_t)ncp * ct * TL_TT);
+    if (d_tbuf != tbuf0) ytile_[0].valid = false;  // reallocated
     if (mode == 0) ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
     ensure(d_trow, cap_trow, (size_t)nwg1 * 3 * ncp);
     const int td = tiled_dens(dens, alpha);
@@ -3704,6 +3745,17 @@ struct DeviceCtx : Evaluator {
     bool oz = y_stage_ != 1 && nf <= 256 && td != DENS_LINEAR && ensure_xsl();
     if (oz) upload_wsl(w, nc);
     oz = oz && xsl_valid_;
+    // the slot of this pass's y fragments (mode 1 writes y only as feature-chunk partials: slot 0)
+    const bool single = ct >= std::max<uint64_t>(n_tiles, 1);
+    int slot = 0;
+    if (mode == 0 && oz && single && multi_ybuf_) {
+      if (ytile_match(0, w, nc)) slot = 0;
+      else if (ytile_match(1, w, nc)) slot = 1;
+      else slot = ytile_last_ ^ 1;
+      if (slot == 1 && !ensure_ybuf2((size_t)ncp * ct * TL_TT)) slot = 0;
+    }
+    if (mode == 0 || nf > kc) ytile_[slot].valid = false;  // this pass writes those y fragments
+    ytarget_ = slot == 1 ? d_ybuf2 : d_tbuf;
     if (!oz) {  // Wᵀ, zero-padded to whole feature chunks (the int8 phase 1 reads W's digit image)
       std::vector<double> wt((size_t)nfp * ncp, 0.0);
       for (size_t i = 0; i < nc; ++i)
@@ -3723,11 +3775,14 @@ struct DeviceCtx : Evaluator {
         default: tiled_launch<DENS_LINEAR>(mode, ks, ncp, alpha, ntl, need_h, nsplit, nwg1, acc, X0, false, t0); break;
       }
     }
-    if (mode == 0 && oz && ct >= std::max<uint64_t>(n_tiles, 1)) {  // one chunk: all of Y stays
-      ytile_valid_ = true;
-      ytile_nc_ = nc;
-      ytile_gen_ = xsl_gen_;
-      ytile_w_.assign(w, w + nc * nf);
+    ytarget_ = nullptr;
+    if (mode == 0 && oz && single) {  // one chunk: all of Y stays
+      YTile& y = ytile_[slot];
+      y.valid = true;
+      y.nc = nc;
+      y.gen = xsl_gen_;
+      y.w.assign(w, w + nc * nf);
+      ytile_last_ = slot;
     }
     const size_t total = (size_t)(mode == 0 ? (need_h ? 2 : 1) * nc * nc : 0) + 3 * nc;
     k_reduce_tiled<<<(total + 255) / 256, 256, 0, stream>>>(d_slab, nsplit, d_trow, nwg1, ncp, (int)nc, need_h,

@@ -86,6 +86,36 @@ def test_multi_ybuf_only_for_the_same_w(pa, rng, monkeypatch):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
+def test_multi_ybuf_two_slots(pa, rng, monkeypatch):
+    """Two full passes keep both Y's (the second W goes to the other slot); a third pass
+    replaces the older one. Every read-back result equals the pass that forms Y."""
+    monkeypatch.delenv("PICARD_MULTI_YBUF", raising=False)
+    nc = nf = 128
+    x = laplace_mix(rng, nf, 5003)
+    ws = [rng.normal(size=(nc, nf)) / np.sqrt(nf) for _ in range(3)]
+    z = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    d = pa.DensityType(1, 0.5)  # exp: the read-back kernel at any Σy² / try count
+    alphas = 0.5 ** np.arange(0, 10)
+    fresh = ctx_with(pa, x)
+    ref = [fresh.eval_loss_multi(w, z, alphas, mu, d) for w in ws]
+    assert fresh.multi_ybuf_passes == 0
+    ctx = ctx_with(pa, x)
+    ctx.eval(ws[0], mu, d, need_h=True)
+    ctx.eval(ws[1], mu, d, need_h=True)
+    got0 = ctx.eval_loss_multi(ws[0], z, alphas, mu, d)
+    got1 = ctx.eval_loss_multi(ws[1], z, alphas, mu, d)
+    assert ctx.multi_ybuf_passes == 2
+    ctx.eval(ws[2], mu, d, need_h=True)  # replaces W0's slot
+    got0b = ctx.eval_loss_multi(ws[0], z, alphas, mu, d)
+    assert ctx.multi_ybuf_passes == 2
+    got1b = ctx.eval_loss_multi(ws[1], z, alphas, mu, d)
+    got2 = ctx.eval_loss_multi(ws[2], z, alphas, mu, d)
+    assert ctx.multi_ybuf_passes == 4
+    for a, b in ((got0, ref[0]), (got1, ref[1]), (got0b, ref[0]), (got1b, ref[1]), (got2, ref[2])):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("n", [100, 256])
 def test_nonortho_fit_multi_ybuf_bit_identical(pa, rng, monkeypatch, n):
     """A non-ortho fit (C4's path: tiled full pass + one multi-try pass per search) lands on
