@@ -38,16 +38,22 @@ std::string rust_e4(double v) {
 }
 
 // ---------------------------------------------------------------- lbfgs.rs
+// Elementwise N×N updates of the host driver split over the team at N ≥ 256 (each element's
+// arithmetic is unchanged, so any split gives the same bits); reductions stay serial.
+constexpr size_t ELEMWISE_PAR = 65536;
+
 Mat compute_direction(const Mat& g, const Mat& h, const std::vector<double>& h_off,
                       const LbfgsMemory& mem, bool ortho) {
   Mat q = g;
   const size_t k = mem.len();
   std::vector<double> alpha_list(k);
+  const long ne = (long)q.a.size();
   for (size_t ii = k; ii-- > 0;) {  // .rev()
     const double alpha = mem.r_list[ii] * dot_sum(mem.s_list[ii], q);
     alpha_list[ii] = alpha;
     const Mat& y = mem.y_list[ii];
-    for (size_t e = 0; e < q.a.size(); ++e) q.a[e] = q.a[e] - alpha * y.a[e];
+#pragma omp parallel for schedule(static) if (ne >= (long)ELEMWISE_PAR)
+    for (long e = 0; e < ne; ++e) q.a[e] = q.a[e] - alpha * y.a[e];
   }
   Mat z;
   if (ortho) {
@@ -63,7 +69,8 @@ Mat compute_direction(const Mat& g, const Mat& h, const std::vector<double>& h_o
     const double beta = mem.r_list[ii] * dot_sum(mem.y_list[ii], z);
     const Mat& s = mem.s_list[ii];
     const double f = alpha_list[ii] - beta;
-    for (size_t e = 0; e < z.a.size(); ++e) z.a[e] = z.a[e] + f * s.a[e];
+#pragma omp parallel for schedule(static) if (ne >= (long)ELEMWISE_PAR)
+    for (long e = 0; e < ne; ++e) z.a[e] = z.a[e] + f * s.a[e];
   }
   for (double& v : z.a) v = -v;
   return z;
@@ -72,6 +79,7 @@ Mat compute_direction(const Mat& g, const Mat& h, const std::vector<double>& h_o
 Mat solve_hessian_system(const Mat& h, const std::vector<double>& h_off, const Mat& g) {
   const size_t n = h.rows;
   Mat r(n, n);
+#pragma omp parallel for schedule(static) if (n * n >= ELEMWISE_PAR)
   for (size_t i = 0; i < n; ++i)
     for (size_t j = 0; j < n; ++j) {
       const double det = h(i, j) * h(j, i) - h_off[i] * h_off[j];
