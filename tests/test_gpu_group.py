@@ -170,6 +170,48 @@ def test_group_fit_reproduces_world1(pa, world, capfd, monkeypatch):
     assert "[picard-screen]" in trace and "[picard-curv]" in trace
 
 
+def test_group_nonortho_fit_rank_identical(pa):
+    """C4's path over the group (world 2): non-orthogonal Picard at N = 100 — the tiled full
+    pass with H and the multi-try pass reading Y back from it (k_multi_loss2_ozy) on every
+    rank. Both ranks bit-identical (lockstep decisions from reduced sums), multi-try passes
+    read Y back, and the fit converges to the fixed point world = 1 reaches: Amari distance to
+    the generating mixing within 1e-6 of it. (Non-orthogonal trajectories are chaotic in the
+    summation order — the shard split changes it — so the iteration counts differ: 124
+    against 90 on the first run.)"""
+    nf, T = 100, 60001
+    cfg = pa.PicardConfig(ortho=False, extended=False, random_state=3, max_iter=200, want_sources=False)
+    ref_ctx = pa.DeviceContext(0)
+    a_mix = ref_ctx.generate(nf, T, 11)
+    sv = pa.Solver(ref_ctx, cfg)
+    while not sv.step():
+        pass
+    ref = sv.finish()
+    sv.close()
+    ref_ctx.close()
+    g = RankGroup(pa, 2, nf, T, seed=11)
+
+    def fit(r, ctx):
+        s = pa.Solver(ctx, cfg)
+        while not s.step():
+            pass
+        out = s.finish()
+        s.close()
+        return out, ctx.multi_ybuf_passes, ctx.comm_stats()
+
+    try:
+        res, err = g.run(fit)
+    finally:
+        g.close()
+    _no_errors(err)
+    (o0, n0, st0), (o1, n1, st1) = res
+    assert np.array_equal(o0.unmixing, o1.unmixing) and o0.n_iterations == o1.n_iterations
+    assert n0 == n1 and n0 > 0 and st0["allreduces"] == st1["allreduces"] and not st0["aborted"]
+    assert o0.converged and ref.converged
+    am0 = pa.utils.amari_distance(o0.full_unmixing(), a_mix)
+    am_ref = pa.utils.amari_distance(ref.full_unmixing(), a_mix)
+    assert abs(am0 - am_ref) <= 1e-6, (am0, am_ref)
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_group_capability_loss_aborts_every_rank(pa, world):
     """One rank loses the int8 digit image the ranks agreed on (pc_ctx_release_caches)
