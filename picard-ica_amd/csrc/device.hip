@@ -4395,12 +4395,16 @@ struct DeviceCtx : Evaluator {
   // k_screen_oz2 (screen.hip): the same statistics and bound as k_screen_oz on the interleaved
   // schedule; PICARD_SCREEN_V2=0 keeps k_screen_oz. false: not available here.
   bool screen_v2_ = !(std::getenv("PICARD_SCREEN_V2") && std::atoi(std::getenv("PICARD_SCREEN_V2")) == 0);
+  bool screen32_ = std::getenv("PICARD_SCREEN32") && std::atoi(std::getenv("PICARD_SCREEN32")) == 1;
   template <int NB>
   bool launch_screen_oz2(double alpha, double* st_rows, int nw = 1) {
     constexpr int NCP = 16 * NB;
-    const int U = screen2_blocks_per_step(NB);
+    // k_screen_oz32 (PICARD_SCREEN32=1): one try at NB = 8, two blocks per step, one workgroup per CU
+    const bool f32form = screen32_ && NB == 8 && nw == 1;
+    const int U = f32form ? 2 : screen2_blocks_per_step(NB);
     const uint64_t n_blocks = (n_local_ + 15) / 16;
-    const uint64_t want = std::min<uint64_t>((uint64_t)2 * n_cu, std::max<uint64_t>((n_blocks + U - 1) / U, 1));
+    const uint64_t want =
+        std::min<uint64_t>((uint64_t)(f32form ? 1 : 2) * n_cu, std::max<uint64_t>((n_blocks + U - 1) / U, 1));
     const uint64_t steps_per_wg = ((n_blocks + U - 1) / U + want - 1) / want;
     const uint64_t bpw = steps_per_wg * U;
     const int nwg = (int)std::max<uint64_t>(1, (n_blocks + bpw - 1) / bpw);
@@ -4417,6 +4421,7 @@ struct DeviceCtx : Evaluator {
     a.ln2_alpha = fm::LN2 / alpha;
     a.bpw = (uint32_t)bpw; a.n_blocks = (uint32_t)n_blocks; a.nwg = nwg; a.partials = part;
     a.nw = nw;
+    a.form32 = f32form;
     HIP_OK(hipEventRecord(ev[1], stream));
     HIP_OK(screen2_launch(NB, a, stream));
     HIP_OK(hipEventRecord(ev[2], stream));

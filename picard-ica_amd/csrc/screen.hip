@@ -247,6 +247,182 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   }
 }
 
+// The same screen on v_mfma_i32_32x32x32_i8 (NB = 8, one try; PICARD_SCREEN32=1): an i8 MFMA of
+// this shape holds its SIMD's vector issue for ≈ 8 of its 32 cycles, so the row terms of step
+// k − 1 (≈ 190 VALU per wave and step) fit in the gaps of step k's 40 MFMAs (1280 cycles), where
+// the 16x16x64 form leaves ≈ 40 % of its row terms exposed (profiles/r05_m: the screen returns
+// about half of a VALU cut as time). One wave per SIMD (4 waves, 256 threads): wave w owns W rows
+// 32w … 32w + 31 of a 32-sample step (two 16-sample image blocks); the diagonal accumulators
+// (4 × 16 int32, double-buffered) take the AGPRs. A operands come from the unchanged digit image:
+// lane l reads the 16-byte item of sample row r = l & 31 (block r >> 4, A-row r & 15) and features
+// 32k + 16(l >> 5) … +15; B operands (W's D ≤ 3 digits) likewise from the W image, once. Output:
+// lane l holds W row 32w + (l & 31) and the 16 sample rows (i & 3) + 8(i >> 2) + 4(l >> 5); the
+// fp32 scale of sample row r of the step is xsf[32·step + r] (k_build_xsf's order is the A-row
+// order). Row terms: row_terms' per-element arithmetic on 4 groups of 4 samples per lane — the
+// grouping the bound's per-4-sample constants assume — so DeviceCtx::screen_at's bound holds as
+// for k_screen_oz2 (the estimate's grouping differs: not bit-identical to it).
+constexpr int S32_U = 2, S32_SLOT = 4 * 2 * 1024, S32_NBUF = 3, S32_SCB = 256;
+constexpr int S32_TILE = SLICES * 2 * 1024;
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ v16i mfma_i8_32(v4i a, v4i b, v16i c) {
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void row_terms32(const v16i (&acc)[4], const float (&sf)[16], float cz, double& l,
+                                            double& g) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float u[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * q + e;
+      const int q01 = acc[0][i] * 256 + acc[1][i], r23 = acc[2][i] * 256 + acc[3][i];
+      u[e] = __builtin_fmaf((float)r23, 0x1p-16f, (float)q01) * sf[i];
+    }
+    float f[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = __builtin_fmaf(__builtin_amdgcn_exp2f(-(__builtin_fabsf(u[e]) * cz)), 0.5f, 0.5f);
+    const float sm = (__builtin_fabsf(u[0]) + __builtin_fabsf(u[1])) + (__builtin_fabsf(u[2]) + __builtin_fabsf(u[3]));
+    l += (double)sm;
+    g += (double)__builtin_amdgcn_logf((f[0] * f[1]) * (f[2] * f[3]));
+  }
+}
+
+template <int FILL>
+__global__ void __launch_bounds__(256, 1)
+k_screen_oz32(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
+              const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
+              double* __restrict__ partials) {
+  constexpr int NCP = 128;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int h = lane >> 5, n = lane & 15, rb16 = 2 * wv + ((lane & 31) >> 4);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* tiles = smem;                                 // [NBUF][U][SLOT]: planes 0–3 of 2 blocks
+  uint8_t* scl = tiles + S32_NBUF * S32_U * S32_SLOT;    // [NBUF][SCB]: 32 fp32 scales
+  const uint32_t b_begin = blockIdx.x * bpw;
+  const uint32_t b_end = b_begin + bpw < n_blocks ? b_begin + bpw : n_blocks;
+  const uint32_t nb = b_begin < b_end ? b_end - b_begin : 0u;
+  const uint32_t nsteps = (nb + S32_U - 1) / S32_U;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(xsl + (size_t)b_begin * S32_TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * S32_TILE)), RSRC_DW3);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
+  // wave w stages pieces 4w … 4w + 3 of every step: block p >> 3, 1-KiB piece p & 7 (planes 0–3 ×
+  // 2 k-steps are the first 8 KiB of a block image); wave 3 also the step's 32 scales
+  const bool scale_wave = wv == 3;
+  auto stage = [&](uint32_t step, int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = 4 * wv + u, bp = p >> 3, q = p & 7;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * S32_U + bp) * S32_SLOT + q * 1024), 16,
+                                               (int)((uint32_t)(bp * S32_TILE + q * 1024 + lane * 16) +
+                                                     step * (uint32_t)(S32_U * S32_TILE)),
+                                               0, 0, 0);
+    }
+    if (scale_wave)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S32_SCB), 4,
+                                               (int)((uint32_t)((lane & 31) * 4) + step * (uint32_t)(S32_U * 64)), 0,
+                                               0, 0);
+  };
+  auto step_barrier = [&]() {
+    if (scale_wave) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // W's D ≤ 3 digits as B operands: lane l = W row 32w + (l & 31), features 32k + 16h … +15
+  v4i wb[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int s2 = k >> 1, g = 2 * (k & 1) + h;
+      wb[a][k] = *(const v4i*)(wsl_g + (size_t)(((rb16 * SLICES + a) * 2 + s2) * 64 + n + 16 * g) * 16);
+    }
+  const double rowscale = __builtin_ldexp(wsc[rb16 * 16 + n], e0 - 8);  // 2^(f_i + E0 − 20)
+  const float cz = __builtin_fabsf(c32) * (float)rowscale;
+  double l = 0.0, g = 0.0;
+  v16i acc[2][4];
+  float sf[2][16];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[1][d] = v16i{};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sf[1][i] = 0.f;
+  stage(0, 0);
+  stage(1, 1);
+  if (scale_wave) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // A item of lane l for (plane b, k-step k): sample row l & 31 → block (l & 31) >> 4, A-row l & 15
+  const int a_off = ((lane & 31) >> 4) * S32_SLOT + n * 16;
+  auto body = [&](uint32_t k, int buf, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value, prv = cur ^ 1;
+    stage(k + 2, buf == 0 ? 2 : buf - 1);  // (k + 2) mod 3; past the end: zeros, never read
+    const uint8_t* tb = tiles + buf * S32_U * S32_SLOT + a_off;
+    v4i xa[2][4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) xa[0][kk] = *(const v4i*)(tb + (kk >> 1) * 1024 + (2 * (kk & 1) + h) * 256);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (b < 3)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          xa[(b + 1) & 1][kk] = *(const v4i*)(tb + ((b + 1) * 2 + (kk >> 1)) * 1024 + (2 * (kk & 1) + h) * 256);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int a = 0; a <= 3 - b; ++a) {
+          const int d = a + b;
+          acc[cur][d] = (b == 0 && kk == 0) ? mfma_i8_32(xa[b & 1][kk], wb[a][kk], v16i{})
+                                            : mfma_i8_32(xa[b & 1][kk], wb[a][kk], acc[cur][d]);
+        }
+    }
+    row_terms32(acc[prv], sf[prv], cz, l, g);
+    {  // this step's 16 scales: sample rows 8q + 4h + 0…3 (q = 0…3)
+      const float* sp = (const float*)(scl + buf * S32_SCB);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *(const float4*)(sp + 8 * q + 4 * h);
+        sf[cur][4 * q + 0] = v.x; sf[cur][4 * q + 1] = v.y; sf[cur][4 * q + 2] = v.z; sf[cur][4 * q + 3] = v.w;
+      }
+    }
+    if constexpr (FILL > 0) {
+#pragma unroll
+      for (int i = 0; i < 40; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, FILL, 0);
+      }
+    }
+    asm volatile("" ::"v"(l), "v"(g));
+    step_barrier();
+  };
+  uint32_t k = 0;
+  int buf = 0;
+  for (; k + 1 < nsteps; k += 2) {
+    body(k, buf, std::integral_constant<int, 0>{});
+    buf = buf == 2 ? 0 : buf + 1;
+    body(k + 1, buf, std::integral_constant<int, 1>{});
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  if (k < nsteps) {
+    body(k, buf, std::integral_constant<int, 0>{});
+    row_terms32(acc[0], sf[0], cz, l, g);
+  } else {
+    row_terms32(acc[1], sf[1], cz, l, g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero pieces past the end: drained
+  double rs_y = l * rowscale;  // Σ|ỹ| (exact scaling)
+  double rs_ll = __builtin_fma(g, ln2_alpha, rs_y);
+  rs_ll += __shfl_xor(rs_ll, 32);
+  rs_y += __shfl_xor(rs_y, 32);
+  if (h == 0) {
+    double* out = partials + (size_t)blockIdx.x * 2 * NCP;  // [Σℓ raw | Σ|ỹ|]
+    out[32 * wv + (lane & 31)] = rs_ll;
+    out[NCP + 32 * wv + (lane & 31)] = rs_y;
+  }
+}
+
 // xsf[16·blk + 4·lk + r] = 2^(e_t − E0) in fp32 for sample t = 16·blk + lk + 4r (the lane's 4
 // samples of k_screen_oz2 contiguous): exact for the image's exponent range (host-checked)
 __global__ void __launch_bounds__(256) k_build_xsf(const double* __restrict__ xsc, uint64_t n, int e0,
@@ -297,7 +473,35 @@ hipError_t launch(const Screen2Args& a, hipStream_t stream) {
 int screen2_blocks_per_step(int nb) { return 8 / nb; }
 uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }
 
+template <int FILL>
+hipError_t screen32_launch_fill(const Screen2Args& a, hipStream_t stream) {
+  constexpr int LDS = S32_NBUF * S32_U * S32_SLOT + S32_NBUF * S32_SCB;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz32<FILL>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  k_screen_oz32<FILL><<<a.nwg, 256, LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha, a.bpw,
+                                                    a.n_blocks, a.partials);
+  return hipGetLastError();
+}
+// PICARD_SCREEN32_FILL (measurement knob): vector instructions per MFMA gap, 0 = compiler order
+hipError_t screen32_launch(const Screen2Args& a, hipStream_t stream) {
+  static const int fill = [] {
+    const char* e = std::getenv("PICARD_SCREEN32_FILL");
+    return e ? std::atoi(e) : 5;
+  }();
+  switch (fill) {
+    case 0: return screen32_launch_fill<0>(a, stream);
+    case 3: return screen32_launch_fill<3>(a, stream);
+    case 8: return screen32_launch_fill<8>(a, stream);
+    default: return screen32_launch_fill<5>(a, stream);
+  }
+}
+
 hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream) {
+  if (a.form32) return nb == 8 && a.nw == 1 ? screen32_launch(a, stream) : hipErrorInvalidValue;
   if (a.nw == 2) return nb == 8 ? launch<8, 2>(a, stream) : launch<4, 2>(a, stream);
   return nb == 8 ? launch<8, 1>(a, stream) : launch<4, 1>(a, stream);
 }
