@@ -193,8 +193,10 @@ void pc_last_teardown(double out[4]);
  * collective. A peer process that exits, or a collective that does not complete within
  * PICARD_COMM_TIMEOUT_S seconds (default 600), aborts the group too. */
 void pc_ctx_abort(pc_ctx* ctx, const char* why);
-/* Free the context's HBM caches (the int8 digit image of X, the kept-Y buffer); later
- * passes run without them (the fp64 Y stage, completion by recomputation). On a rank
+/* Free the context's HBM caches (the int8 digit image of X, the kept-Y buffer of split
+ * evaluation, the second y-fragment buffer of the multi-try pass; the first y-fragment
+ * slot, inside the tiled pass's buffer, is invalidated); later passes run without them
+ * (the fp64 Y stage, completion and multi-try Y by recomputation). On a rank
  * whose group agreed to use the digit image this makes its next screened try fail —
  * and abort the group — rather than let the ranks diverge. */
 int pc_ctx_release_caches(pc_ctx* ctx, char* err, size_t errlen);

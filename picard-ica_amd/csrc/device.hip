@@ -3125,7 +3125,13 @@ struct DeviceCtx : Evaluator {
           const double bound = 1.0 / std::sqrt(alpha * 2.718281828459045) * (1.0 + 1e-12);
           psc = std::ldexp(1.0, 46 - (std::ilogb(bound) + 1));
         }
-        auto kg8x = k_eval_fused_g8x<D, Q>;
+        auto kg8x = k_eval_fused_g8x<D, Q, 0>;
+        switch (g8x_var_) {
+          case 1: kg8x = k_eval_fused_g8x<D, Q, 1>; break;
+          case 4: kg8x = k_eval_fused_g8x<D, Q, 4>; break;
+          case 5: kg8x = k_eval_fused_g8x<D, Q, 5>; break;
+          default: break;
+        }
         lds_attr((const void*)kg8x, G8X_LDS);
         HIP_OK(hipEventRecord(ev[1], stream));
         kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
@@ -3733,10 +3739,12 @@ struct DeviceCtx : Evaluator {
     const int nto = (ncp / 16 + 7) / 8;
     const int nsplit = (int)std::max<uint64_t>(1, std::min<uint64_t>(ct, (uint64_t)(2 * n_cu / (nto * nto))));
     // y buffer: always in mode 0; in mode 1 only to carry partial y across feature chunks
-    const double* tbuf0 = d_tbuf;
+    // reallocation is detected by the capacity, not the address: the allocator may hand the
+    // freed buffer's address straight back, and the kept Y in it is gone either way
+    const size_t tcap0 = cap_tbuf;
     if (mode == 0) ensure(d_tbuf, cap_tbuf, (size_t)narr * ncp * ct * TL_TT);
     else if (nf > kc) ensure(d_tbuf, cap_tbuf, (size_t)ncp * ct * TL_TT);
-    if (d_tbuf != tbuf0) ytile_[0].valid = false;  // reallocated
+    if (cap_tbuf != tcap0) ytile_[0].valid = false;  // reallocated
     if (mode == 0) ensure(d_slab, cap_slab, (size_t)nsplit * (need_h ? 2 : 1) * ncp * ncp);
     ensure(d_trow, cap_trow, (size_t)nwg1 * 3 * ncp);
     const int td = tiled_dens(dens, alpha);
@@ -3834,6 +3842,8 @@ struct DeviceCtx : Evaluator {
   // d_wsc[256 …] are valid for the W image and the digit image whose largest sample exponent is
   // g8_emax_
   int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) == 0) ? 1 : 0;
+  // schedule variant of k_eval_fused_g8x (fused_g8x.inc; the same bits in every variant)
+  const int g8x_var_ = std::getenv("PICARD_G8X_VAR") ? std::atoi(std::getenv("PICARD_G8X_VAR")) : 0;
   bool g8_scales_ok_ = false;
 
   int g8_emax_ = INT_MIN;
@@ -5016,6 +5026,16 @@ void device_ctx_release_caches(Evaluator* e) {
     d->d_ybuf = nullptr;
     d->cap_ybuf = 0;
   }
+  // the multi-try pass's y fragments: slot 1's buffer is freed, and neither slot may be read
+  // again (slot 0 lives in d_tbuf, which stays allocated but is no longer a promised cache)
+  if (d->d_ybuf2) {
+    d->sync();
+    HIP_OK(d->t_free(d->d_ybuf2));
+    d->d_ybuf2 = nullptr;
+    d->cap_ybuf2 = 0;
+  }
+  d->ytile_[0].valid = false;
+  d->ytile_[1].valid = false;
 }
 void device_ctx_load(Evaluator* e, const double* x, uint64_t nf, uint64_t nl, uint64_t nt, uint64_t t0) {
   static_cast<DeviceCtx*>(e)->load(x, nf, nl, nt, t0);

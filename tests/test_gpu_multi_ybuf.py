@@ -116,6 +116,57 @@ def test_multi_ybuf_two_slots(pa, rng, monkeypatch):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
+def test_multi_ybuf_slot0_dropped_when_buffer_grows(pa, rng, monkeypatch):
+    """A full pass that grows the tiled pass's buffer (exp with H stores ψ′ as a third array,
+    tanh forms it from ψ) frees slot 0's Y even when the allocator returns the same address:
+    a multi-try pass at slot 0's old W must then form Y, and equal a fresh context's result."""
+    monkeypatch.delenv("PICARD_MULTI_YBUF", raising=False)
+    nc = nf = 128
+    x = laplace_mix(rng, nf, 4099)
+    w0, w1, w2 = (rng.normal(size=(nc, nf)) / np.sqrt(nf) for _ in range(3))
+    z = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    th, ex = pa.DensityType(0, 1.0), pa.DensityType(1, 0.5)
+    alphas = 0.5 ** np.arange(0, 10)
+    fresh = ctx_with(pa, x)
+    ref1 = fresh.eval_loss_multi(w1, z, alphas, mu, ex)
+    ref2 = fresh.eval_loss_multi(w2, z, alphas, mu, ex)
+    ctx = ctx_with(pa, x)
+    ctx.eval(w0, mu, th, need_h=True)   # y, ψ: Y(w0) in slot 1 (the second y buffer)
+    ctx.eval(w1, mu, th, need_h=True)   # Y(w1) in slot 0 (inside the tiled pass's buffer)
+    ctx.eval(w2, mu, ex, need_h=True)   # y, ψ, ψ′: that buffer grows; Y(w2) replaces Y(w0) in slot 1
+    got1 = ctx.eval_loss_multi(w1, z, alphas, mu, ex)   # slot 0 is gone: forms Y
+    got2 = ctx.eval_loss_multi(w2, z, alphas, mu, ex)   # reads slot 1 back
+    assert ctx.multi_ybuf_passes == 1
+    for a, b in ((got1, ref1), (got2, ref2)):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_release_caches_drops_y_fragments(pa, rng, monkeypatch):
+    """pc_ctx_release_caches frees the second y buffer and invalidates both slots: a multi-try
+    pass at a W whose Y was kept forms it again, with the bits of a context that never kept it
+    (both without the digit image, which release_caches frees for good)."""
+    monkeypatch.delenv("PICARD_MULTI_YBUF", raising=False)
+    nc = nf = 128
+    x = laplace_mix(rng, nf, 3001)
+    ws = [rng.normal(size=(nc, nf)) / np.sqrt(nf) for _ in range(2)]
+    z = rng.normal(size=(nc, nf)) / np.sqrt(nf)
+    mu = x.mean(axis=1)
+    d = pa.DensityType(1, 0.5)
+    alphas = 0.5 ** np.arange(0, 10)
+    fresh = ctx_with(pa, x)
+    fresh.release_caches()
+    ref = [fresh.eval_loss_multi(w, z, alphas, mu, d) for w in ws]
+    ctx = ctx_with(pa, x)
+    for w in ws:
+        ctx.eval(w, mu, d, need_h=True)
+    ctx.release_caches()
+    got = [ctx.eval_loss_multi(w, z, alphas, mu, d) for w in ws]
+    assert ctx.multi_ybuf_passes == 0
+    for a, b in zip(got, ref):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("n", [100, 256])
 def test_nonortho_fit_multi_ybuf_bit_identical(pa, rng, monkeypatch, n):
     """A non-ortho fit (C4's path: tiled full pass + one multi-try pass per search) lands on
