@@ -2695,6 +2695,7 @@ struct DeviceCtx : Evaluator {
   size_t kept_nc = 0; int kept_nb = 0;
   hipEvent_t ev[4];
   double last_kernel_ms = 0, last_call_ms = 0;
+  double last_pass_kernel_ms() const override { return last_kernel_ms; }
   double sum_kernel_ms = 0, sum_call_ms = 0;
   uint64_t n_kernel = 0;
   // Pinned host staging for the per-pass uploads (W image, W digit image): the copy is
@@ -3125,13 +3126,7 @@ struct DeviceCtx : Evaluator {
           const double bound = 1.0 / std::sqrt(alpha * 2.718281828459045) * (1.0 + 1e-12);
           psc = std::ldexp(1.0, 46 - (std::ilogb(bound) + 1));
         }
-        auto kg8x = k_eval_fused_g8x<D, Q, 0>;
-        switch (g8x_var_) {
-          case 1: kg8x = k_eval_fused_g8x<D, Q, 1>; break;
-          case 4: kg8x = k_eval_fused_g8x<D, Q, 4>; break;
-          case 5: kg8x = k_eval_fused_g8x<D, Q, 5>; break;
-          default: break;
-        }
+        auto kg8x = k_eval_fused_g8x<D, Q>;
         lds_attr((const void*)kg8x, G8X_LDS);
         HIP_OK(hipEventRecord(ev[1], stream));
         kg8x<<<nwg, G8X_THREADS, G8X_LDS, stream>>>(bpw, n_blocks, part, d_xsl, d_xsc, d_wsl, d_wsc, alpha, psc);
@@ -3842,8 +3837,6 @@ struct DeviceCtx : Evaluator {
   // d_wsc[256 …] are valid for the W image and the digit image whose largest sample exponent is
   // g8_emax_
   int g_stage_ = (std::getenv("PICARD_G8") && std::atoi(std::getenv("PICARD_G8")) == 0) ? 1 : 0;
-  // schedule variant of k_eval_fused_g8x (fused_g8x.inc; the same bits in every variant)
-  const int g8x_var_ = std::getenv("PICARD_G8X_VAR") ? std::atoi(std::getenv("PICARD_G8X_VAR")) : 0;
   bool g8_scales_ok_ = false;
 
   int g8_emax_ = INT_MIN;
@@ -3962,6 +3955,23 @@ struct DeviceCtx : Evaluator {
     return true;
   }
   double xsc_sum_ = 0.0;
+  // The digit G stage scales every y of a row by one power of two set by the image's LARGEST
+  // sample exponent emax, so a typical sample keeps 2^(emax − e_typ) fewer bits of y (its X
+  // digits carry their own 2^e_t; y's fixed point does not). Its G error grows by that factor
+  // (measured, tests/test_gpu_g8.py: ≈ 1e-13 relative at T ≈ 5e3 for Δe = 0.8, 1.1e-12 for
+  // Δe = 3.8; falling as 1/√T), so the stage runs only while Δe = emax − log2(mean of 2^e_t over
+  // the valid samples) ≤ G8_SPREAD_MAX + ½·log2(T / 5000) (one more bit per 4× samples: at most
+  // ≈ 5e-13 at any T) — samples 8× the typical one at T ≈ 5e3 put G back on fp64 MFMA (same
+  // all-reduce: no agreement needed). The bench mixture: Δe ≈ 0.9 at T = 2e5 (C3 shards: ≤ 10).
+  static constexpr int G8_SPREAD_MAX = 3;
+  bool g8_spread_ok(int emax) const {
+    if (n_local_ == 0) return true;
+    // padding samples carry the scale 1 exactly (k_slice_x): remove them from the sum
+    const double valid = xsc_sum_ - (double)(ldx - n_local_);
+    if (!(valid > 0.0)) return false;
+    const double extra = std::floor(std::fmax(0.0, 0.5 * std::log2((double)n_local_ / 5000.0)));
+    return (double)emax - std::log2(valid / (double)n_local_) <= (double)G8_SPREAD_MAX + extra;
+  }
   // exponent range of the digit image's sample scales 2^e_t (the fp32 screen's range check)
   int xsc_emin_ = 0, xsc_emax_ = 0;
   bool xsc_range_ok_ = false;
@@ -4020,7 +4030,7 @@ struct DeviceCtx : Evaluator {
     // the 6-digit range reaches 0.996·2^47); zero rows (padding) get 1
     g8_scales_ok_ = false;
     g8_emax_ = INT_MIN;
-    if (nc <= 128 && emax != INT_MIN) {
+    if (nc <= 128 && emax != INT_MIN && g8_spread_ok(emax)) {
       bool ok = true;
       for (size_t j = 0; j < 128; ++j) {
         double s1 = 0.0;
@@ -4823,15 +4833,21 @@ struct DeviceCtx : Evaluator {
     // an error: the host sweeps run instead (PICARD_TEST_JADE_REFUSE=1 refuses every launch,
     // a test hook).
     const bool coop_launch = (coll_ && std::strcmp(coll_->kind(), "local") == 0) || ctxs_on_device(device) > 1;
+    // test hooks of the bounded wait (jade_sweeps.inc): a lower poll cap, a withheld publish
+    unsigned poll_cap = JS_POLL_CAP;
+    int stall_wg = -1;
+    if (const char* e = std::getenv("PICARD_TEST_JADE_POLL_CAP")) poll_cap = (unsigned)std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("PICARD_TEST_JADE_STALL")) stall_wg = std::atoi(e);
     hipError_t le = hipSuccess;
     if (std::getenv("PICARD_TEST_JADE_REFUSE") && std::atoi(std::getenv("PICARD_TEST_JADE_REFUSE")) != 0) {
       le = hipErrorCooperativeLaunchTooLarge;
     } else if (coop_launch) {
-      void* args[] = {&d_a, &np_i, &n_i, &npos_i, &mw_i, &it_i, &tol_d, &d_v, &d_g, &d_sw, &d_th, (void*)&theta_cap, &seq0, &max_pairs};
+      void* args[] = {&d_a, &np_i, &n_i,  &npos_i, &mw_i, &it_i, &tol_d, &d_v,      &d_g,
+                      &d_sw, &d_th, (void*)&theta_cap, &seq0, &max_pairs, &poll_cap, &stall_wg};
       le = hipLaunchCooperativeKernel(kern, dim3((unsigned)G), dim3((unsigned)th), args, (unsigned)lds, stream);
     } else {
       k_jade_sweeps<JS_THREADS><<<dim3((unsigned)G), dim3((unsigned)th), lds, stream>>>(
-          d_a, np_i, n_i, npos_i, mw_i, it_i, tol_d, d_v, d_g, d_sw, d_th, theta_cap, seq0, max_pairs);
+          d_a, np_i, n_i, npos_i, mw_i, it_i, tol_d, d_v, d_g, d_sw, d_th, theta_cap, seq0, max_pairs, poll_cap, stall_wg);
       le = hipGetLastError();
     }
     last_jade_coop_ = coop_launch;

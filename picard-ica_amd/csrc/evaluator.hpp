@@ -72,6 +72,9 @@ class Evaluator {
       f();
     }
   }
+  // kernel time (ms) of the last pass this evaluator ran, < 0 when it does not know: the caller
+  // books the part of an overlap hook that outlasted the pass as host time
+  virtual double last_pass_kernel_ms() const { return -1.0; }
   virtual uint64_t n_features() const = 0;
   virtual uint64_t n_samples() const = 0;  // global T over all ranks
   // true for a detached shard (world > 1, no communicator): every statistic is

@@ -540,6 +540,16 @@ static double screen_cost_ratio(size_t nc, uint64_t t) {
   return (18.6 * w + 0.08) / (84.0 * w + 0.10);
 }
 
+// The device share of an evaluator call that ran `hook_ms` of the caller's host work while its
+// pass was in flight (Evaluator::overlap_): the whole call while the hook hid behind the pass;
+// once the hook outlasts the pass's kernel time, the excess is host time. Without a
+// kernel time the call counts as device time.
+double Solver::device_share(double call_ms, double hook_ms) const {
+  const double k = ev_->last_pass_kernel_ms();
+  if (!(hook_ms > 0.0) || !(k >= 0.0)) return call_ms;
+  return std::fmin(call_ms, std::fmax(call_ms - hook_ms, k));
+}
+
 Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool multi_first,
                                      bool first_loss_only, bool full_first) {  // core.rs:99-150
   // Evaluation schedule: a try is a full fused pass, or a loss-only pass
@@ -628,11 +638,16 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         Evaluator* ev;
         ~HookGuard() { ev->overlap_ = nullptr; }
       } hook_guard{ev_};
+      double hook_ms = 0.0;  // the overlapped host work: booked as host time where it outlasts the pass
       if (bounded) form_tries(0, nj);
-      else ev_->overlap_ = [&, nj] { form_tries(0, nj); };
+      else ev_->overlap_ = [&, nj] {
+        const double th = now_ms();
+        form_tries(0, nj);
+        hook_ms = now_ms() - th;
+      };
       const bool multi_ran = bounded || ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr,
                                                              cfg_.density, alphas.data(), (int)nj, ll.data(), y2.data());
-      eval_ms_ += now_ms() - tmp0;  // the multi-try pass is device time
+      eval_ms_ += device_share(now_ms() - tmp0, hook_ms);  // the multi-try pass is device time
       ev_->run_overlap();  // (not run by the evaluator)
       if (!multi_ran) r.w = wj[0];  // try k on its own pass (below)
       if (multi_ran) {
@@ -692,11 +707,16 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           nj = na - j0;  // the remaining tries in one more pass
           ++multi_second_passes_;
           const double tmp1 = now_ms();
-          ev_->overlap_ = [&, j0, nj] { form_tries(j0, nj); };
+          hook_ms = 0.0;
+          ev_->overlap_ = [&, j0, nj] {
+            const double th = now_ms();
+            form_tries(j0, nj);
+            hook_ms = now_ms() - th;
+          };
           if (!ev_->eval_loss_multi(wt.data(), zt.data(), n, has_mu_ ? mu_.data() : nullptr, cfg_.density,
                                     alphas.data() + j0, (int)nj, ll.data() + j0 * n, y2.data() + j0 * n))
             throw computation_error("multi-try pass refused after an earlier one ran");
-          eval_ms_ += now_ms() - tmp1;
+          eval_ms_ += device_share(now_ms() - tmp1, hook_ms);
           ev_->run_overlap();
         }
         // no try accepted: the caller evaluates the last try in full if it keeps it — unless

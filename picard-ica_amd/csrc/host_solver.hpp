@@ -78,6 +78,7 @@ class Solver {
   // det_sg / det_la: sign and log|det w| when the search already formed them (NaN: not formed)
   struct LsResult { bool success; Mat w; EvalStats stats; double loss; Mat step; bool partial; size_t tries; bool needs_full;
                     bool screened_out; double det_sg = std::numeric_limits<double>::quiet_NaN(), det_la = 0.0; };
+  double device_share(double call_ms, double hook_ms) const;
   LsResult line_search(const Mat& direction, size_t tries, bool multi_first, bool first_loss_only,
                        bool full_first = false);
   void init_core();

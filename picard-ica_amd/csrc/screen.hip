@@ -83,8 +83,7 @@ struct S2 {
   static constexpr int lds() { return NBUF * U * SLOT + NBUF * SCB + NW * U * NCP * 2 * 8; }
 };
 
-// FILL & 15: vector instructions scheduled after each MFMA (0: no schedule groups, the compiler's
-// order); FILL & 16: the digit planes' LDS-DMA with the non-temporal cache policy.
+// FILL: vector instructions scheduled after each MFMA (0: no schedule groups, the compiler's order).
 // NW = 2: two tries at once (the W image's row blocks NB … 2·NB − 1 and row scales 16·NB … hold
 // the second W): every X operand read and staged once for both, each W's row terms in the
 // arithmetic and order of NW = 1 (so each W's sums are bit-identical to its own screen), partials
@@ -125,7 +124,7 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   const bool scale_wave = wv == 7;
   auto stage = [&](uint32_t step, int buf) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bp) * SLOT + q * 1024), 16,
-                                             (int)(voff_x + step * (uint32_t)(U * TILE)), 0, 0, (FILL & 16) ? 2 : 0);
+                                             (int)(voff_x + step * (uint32_t)(U * TILE)), 0, 0, 0);
     if (scale_wave)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB), 4,
                                                (int)(voff_s + step * (uint32_t)(U * 64)), 0, 0, 0);
@@ -196,11 +195,11 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
     for (int w = 0; w < NW; ++w) row_terms(acc[prv][w], sf[prv], cz[w], l[w], g[w]);
     sf[cur] = *(const f4v*)(scl + buf * S::SCB + h * 64 + lk * 16);
     // one MFMA, then FILL vector instructions, over the 10·KSO·NW MFMAs of the step
-    if constexpr ((FILL & 15) > 0) {
+    if constexpr (FILL > 0) {
 #pragma unroll
       for (int i = 0; i < 10 * KSO * NW; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, FILL & 15, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, FILL, 0);
       }
     }
     // the row sums are complete here: keeps the row terms in this block (between the MFMAs)
@@ -460,17 +459,8 @@ int fill_knob() {
   }();
   return v;
 }
-// PICARD_SCREEN2_NT=1 (measurement knob): the digit planes' DMA with the non-temporal policy
-bool nt_knob() {
-  static const bool v = [] {
-    const char* e = std::getenv("PICARD_SCREEN2_NT");
-    return e && std::atoi(e) == 1;
-  }();
-  return v;
-}
 template <int NB, int NW>
 hipError_t launch(const Screen2Args& a, hipStream_t stream) {
-  if (nt_knob()) return launch_fill<NB, 17, NW>(a, stream);
   switch (fill_knob()) {
     case 0: return launch_fill<NB, 0, NW>(a, stream);
     case 2: return launch_fill<NB, 2, NW>(a, stream);

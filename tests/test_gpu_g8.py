@@ -159,6 +159,30 @@ def test_g8_non_finite_falls_back(pa, rng):
     assert np.isnan(got["G"]).all() and np.isnan(got["ll"]).all()
 
 
+@pytest.mark.parametrize("scale,digit_g", [(2.0, True), (8.0, False), (1e5, False)])
+@pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 1.0)])
+def test_g8_outlying_samples(pa, po, rng, scale, digit_g, dens):
+    """A few samples far above the typical one: y's fixed point is set by the
+    largest sample exponent, so its G error grows with the spread Δe between that exponent and
+    the typical one (this mixture: Δe ≈ 0.8 clean, ≈ 1.8 / 3.8 / 10.7 with three samples 2× /
+    8× / 1e5× the rest; the digit G stage measured 1.1e-12 at Δe = 3.8). The stage keeps only
+    Δe ≤ 3 at this T (DeviceCtx::g8_spread_ok); G is within 1e-12 of the oracle either way."""
+    n, t = 128, 5003
+    x = laplace_mix(rng, n, t)
+    x[:, [17, 2500, 4999]] *= scale
+    ctx = pa.DeviceContext(0)
+    ctx.set_g_stage("auto")
+    ctx.load(x)
+    w = rng.normal(size=(n, n)) / np.sqrt(n)
+    mu = x.mean(axis=1)
+    d = dens_of(pa, dens)
+    got = ctx.eval(w, mu, d, False, need_y2=True)
+    assert ctx.g8_passes == (1 if digit_g else 0)
+    want = po.pass_stats(w, mu, x, density_of(po, d), False)
+    for k in want:
+        assert rel_err(got[k], want[k]) <= TOL, (k, rel_err(got[k], want[k]))
+
+
 def test_g8_fit_matches_f64_g_fit(pa, rng):
     """A Picard-O fit on the digit G stage against the same fit on the fp64 G stage: same
     iterations ±2, unmixing within 1e-6 (G differs only by rounding)."""

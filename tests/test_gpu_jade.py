@@ -115,6 +115,32 @@ def test_jade_refused_launch_leaks_nothing(pa, c5_small, c1_data, monkeypatch):
     assert np.array_equal(refused.unmixing, host.unmixing)
 
 
+@pytest.mark.parametrize("stall_wg", [0, 5])
+def test_jade_stalled_grid_aborts_and_falls_back(pa, c5_small, monkeypatch, stall_wg):
+    """The device sweeps' bounded wait: a workgroup that never publishes a pair's
+    partial sums (PICARD_TEST_JADE_STALL, with a low poll cap PICARD_TEST_JADE_POLL_CAP) must end
+    the whole grid with the abort flag — every wave reaches it, the launch returns — and the
+    context then runs the host sweeps: where='device' raises Unsupported, a default call gives
+    the host sweeps' V bit for bit, and the device sweeps work again once the hook is cleared."""
+    import time
+    ctx, k, mu, _, _ = c5_small
+    monkeypatch.setenv("PICARD_JADE_MAX_PAIRS", str(PREFIX))
+    wh = ctx.jade(k, mu, max_iter=1, where="host")[0]
+    wd = ctx.jade(k, mu, max_iter=1, where="device")[0]
+    monkeypatch.setenv("PICARD_TEST_JADE_POLL_CAP", "20000")
+    monkeypatch.setenv("PICARD_TEST_JADE_STALL", str(stall_wg))
+    t0 = time.perf_counter()
+    with pytest.raises(pa.Unsupported):
+        ctx.jade(k, mu, max_iter=1, where="device")
+    w, _, _, on_dev = ctx.jade(k, mu, max_iter=1)
+    assert time.perf_counter() - t0 < 30.0
+    assert not on_dev and np.array_equal(w, wh)
+    monkeypatch.delenv("PICARD_TEST_JADE_STALL")
+    monkeypatch.delenv("PICARD_TEST_JADE_POLL_CAP")
+    w2, _, _, on_dev2 = ctx.jade(k, mu, max_iter=1, where="device")
+    assert on_dev2 and np.array_equal(w2, wd)
+
+
 @pytest.mark.parametrize("host", [False, True])
 def test_jade_verbose_lines(pa, c1_data, capfd, monkeypatch, host):
     """jade.rs:57-66: the 'JADE iteration N: max angle' line every 10 sweeps, from the
