@@ -53,8 +53,9 @@ extern "C" {
  * operator boundary (they no longer abort a rank group). 5: pc_ctx_comm_timing,
  * pc_solver_timing, pc_solver_setup_timing, pc_ctx_alloc_stats, pc_last_teardown,
  * pc_device_mem_info. 6: pc_ctx_eval_loss_screen2 (paired screen), pc_ctx_screen_tries.
+ * 7: pc_ctx_matrix_exp, pc_matrix_exp (no layout change).
  * pc_abi_version() returns the revision the library was built with. */
-#define PC_ABI_VERSION 6
+#define PC_ABI_VERSION 7
 
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {
@@ -392,6 +393,13 @@ uint64_t pc_ctx_g8_passes(const pc_ctx* ctx);
  * the same int8 digit products; PICARD_MULTI_YBUF=0 in the environment turns this off for new
  * contexts) */
 uint64_t pc_ctx_multi_ybuf_passes(const pc_ctx* ctx);
+/* expm(a) of an n × n row-major a (math.rs:38-74 matrix_exp, the map W ← expm(α·D)·W of an
+ * orthogonal line-search try, core.rs:118-125) as the solver forms try 1's map: on the device
+ * (k_expm_ps) with the bits of pc_matrix_exp. Returns PC_ERR_UNSUPPORTED where the device leaves
+ * it to the host (n not a multiple of 32 in [32, 128], a series the reference caps at 30 terms,
+ * more than 48 squarings, PICARD_DEVICE_EXPM=0). pc_matrix_exp: the host's matrix_exp. */
+int pc_ctx_matrix_exp(pc_ctx* ctx, const double* a, uint64_t n, double* out, char* err, size_t errlen);
+void pc_matrix_exp(const double* a, uint64_t n, double* out);
 /* The line-search screen itself: ll_out[i] = Σℓ of row i from the 4 leading digit
  * diagonals, bound_out[i] ≥ |Σℓ_exact − ll_out[i]| (rounding included), both summed
  * over ranks. Returns PC_ERR_UNSUPPORTED when the context has no screen for this

@@ -205,6 +205,8 @@ def _load():
         "pc_ctx_set_g_stage": (C.c_int, [vp, i32]),
         "pc_ctx_g8_passes": (u64, [vp]),
         "pc_ctx_multi_ybuf_passes": (u64, [vp]),
+        "pc_ctx_matrix_exp": (i32, [vp, d, u64, d, cp, sz]),
+        "pc_matrix_exp": (None, [d, u64, d]),
         "pc_ctx_screen_stats": (None, [vp, d, P(u64), i32]),
         "pc_ctx_eval_loss_screen": (C.c_int, [vp, d, u64, d, _Density, d, d, cp, sz]),
         "pc_ctx_eval_loss_screen2": (C.c_int, [vp, d, d, u64, d, _Density, d, d, d, d, cp, sz]),
@@ -236,7 +238,7 @@ EXPORTED = [
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_set_g_stage", "pc_ctx_g8_passes", "pc_ctx_multi_ybuf_passes", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_ctx_screen_tries", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_set_g_stage", "pc_ctx_g8_passes", "pc_ctx_multi_ybuf_passes", "pc_ctx_matrix_exp", "pc_matrix_exp", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_ctx_screen_tries", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_solver_timing", "pc_solver_setup_timing", "pc_fit_with_evaluator",
 ]
 
@@ -751,6 +753,17 @@ class DeviceContext:
     def g8_passes(self) -> int:
         """fused passes whose G stage ran on int8 digits (pc_ctx_g8_passes)."""
         return int(lib.pc_ctx_g8_passes(self.h))
+
+    def matrix_exp(self, a) -> np.ndarray:
+        """pc_ctx_matrix_exp: expm(a) on the device with the host matrix_exp's bits (try 1's
+        map of an orthogonal line search); raises Unsupported where the device leaves it to the
+        host."""
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        n = a.shape[0]
+        out = np.empty((n, n))
+        err = _errbuf()
+        _raise(lib.pc_ctx_matrix_exp(self.h, _ptr(a), n, _ptr(out), err, len(err)), err)
+        return out
 
     @property
     def multi_ybuf_passes(self) -> int:

@@ -513,6 +513,19 @@ int pc_ctx_set_g_stage(pc_ctx* c, int32_t mode) {
 uint64_t pc_ctx_g8_passes(const pc_ctx* c) { return device_ctx_g8_passes(c->ev.get()); }
 uint64_t pc_ctx_multi_ybuf_passes(const pc_ctx* c) { return device_ctx_multi_ybuf_passes(c->ev.get()); }
 
+int pc_ctx_matrix_exp(pc_ctx* c, const double* a, uint64_t n, double* out, char* err, size_t errlen) {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
+    if (!c->ev->device_matrix_exp(a, n, out)) throw unsupported("device matrix exponential for this shape / series");
+  });
+}
+
+void pc_matrix_exp(const double* a, uint64_t n, double* out) {  // math.rs:38-74
+  Mat A(n, n);
+  std::memcpy(A.data(), a, n * n * sizeof(double));
+  const Mat e = matrix_exp(A);
+  std::memcpy(out, e.data(), n * n * sizeof(double));
+}
+
 int pc_ctx_eval_loss_screen(pc_ctx* c, const double* w, uint64_t nc, const double* mu, pc_density density,
                             double* ll_out, double* bound_out, char* err, size_t errlen) {
   return guarded_on(c->ev.get(), err, errlen, [&] {

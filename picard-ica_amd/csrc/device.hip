@@ -31,6 +31,7 @@
 #include "screen2.hpp"
 #include "evaluator.hpp"
 #include "host_linalg.hpp"
+#include "expm_plan.hpp"
 
 namespace pcamd {
 size_t jade_max_pairs();  // host_solver.cpp (PICARD_JADE_MAX_PAIRS test hook)
@@ -2547,6 +2548,7 @@ __device__ __forceinline__ double laplace_of(uint64_t st) {
 }
 
 #include "jade_sweeps.inc"
+#include "expm.inc"  // try 1's map expm(α·D) on the device, the host's bits (after the granules)
 
 // Cumulant matrices for the sweeps from the lexicographic fourth moments M (np × np, pair
 // index m ↔ (i, j), i ≤ j, the order of jade_warm_start's pidx and pos): A[pos(k,l)][m] =
@@ -2764,13 +2766,13 @@ struct DeviceCtx : Evaluator {
     coll_.reset();
     for (double* p : {X, d_w, d_mu, d_part, d_stats, d_chunk, d_ybuf, d_tbuf, d_ybuf2, d_slab, d_trow, d_shift_sum, d_shift_part, d_wys, d_src, d_jade})
       if (p) (void)t_free(p);
-    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc, (void*)d_xsf})  // d_wsl lies inside d_wsc's allocation
+    for (void* p : {(void*)d_xsl, (void*)d_xsc, (void*)d_wsc, (void*)d_xsf, (void*)d_xm})  // d_wsl lies inside d_wsc's allocation
       if (p) (void)t_free(p);
     for (auto& e : ev) (void)hipEventDestroy(e);
     for (auto& pr : ar_ev_)
       for (auto& e : pr)
         if (e) (void)hipEventDestroy(e);
-    for (PinSlot* sl : {&pin_w_, &pin_wsl_, &pin_out_, &pin_in_, &pin_direct_}) {
+    for (PinSlot* sl : {&pin_w_, &pin_wsl_, &pin_out_, &pin_in_, &pin_direct_, &pin_xm_, &pin_xmo_}) {
       if (sl->pending) (void)hipEventSynchronize(sl->ev);
       if (sl->p) (void)hipHostFree(sl->p);
       if (sl->ev) (void)hipEventDestroy(sl->ev);
@@ -3959,18 +3961,18 @@ struct DeviceCtx : Evaluator {
   // sample exponent emax, so a typical sample keeps 2^(emax − e_typ) fewer bits of y (its X
   // digits carry their own 2^e_t; y's fixed point does not). Its G error grows by that factor
   // (measured, tests/test_gpu_g8.py: ≈ 1e-13 relative at T ≈ 5e3 for Δe = 0.8, 1.1e-12 for
-  // Δe = 3.8; falling as 1/√T), so the stage runs only while Δe = emax − log2(mean of 2^e_t over
-  // the valid samples) ≤ G8_SPREAD_MAX + ½·log2(T / 5000) (one more bit per 4× samples: at most
-  // ≈ 5e-13 at any T) — samples 8× the typical one at T ≈ 5e3 put G back on fp64 MFMA (same
-  // all-reduce: no agreement needed). The bench mixture: Δe ≈ 0.9 at T = 2e5 (C3 shards: ≤ 10).
-  static constexpr int G8_SPREAD_MAX = 3;
+  // Δe ≈ 3.8; falling as 1/√T), so the stage runs only while Δe = emax − log2(mean of 2^e_t over
+  // the valid samples) ≤ G8_SPREAD_MAX + ⌊½·log2(T / 5000)⌋ (one more bit per 4× samples: at most
+  // ≈ 4e-13 at any T) — samples 16× the typical one at T ≈ 5e3 put G back on fp64 MFMA (same
+  // all-reduce: no agreement needed). The bench mixture: Δe ≈ 0.9 at T = 2e5 (C3 shards: ≤ 7.5).
+  static constexpr double G8_SPREAD_MAX = 2.5;
   bool g8_spread_ok(int emax) const {
     if (n_local_ == 0) return true;
     // padding samples carry the scale 1 exactly (k_slice_x): remove them from the sum
     const double valid = xsc_sum_ - (double)(ldx - n_local_);
     if (!(valid > 0.0)) return false;
     const double extra = std::floor(std::fmax(0.0, 0.5 * std::log2((double)n_local_ / 5000.0)));
-    return (double)emax - std::log2(valid / (double)n_local_) <= (double)G8_SPREAD_MAX + extra;
+    return (double)emax - std::log2(valid / (double)n_local_) <= G8_SPREAD_MAX + extra;
   }
   // exponent range of the digit image's sample scales 2^e_t (the fp32 screen's range check)
   int xsc_emin_ = 0, xsc_emax_ = 0;
@@ -4871,6 +4873,62 @@ struct DeviceCtx : Evaluator {
     return true;
   }
   bool last_jade_coop_ = false;
+
+  // expm(a) (n × n) by k_expm_ps (expm.inc): the host matrix_exp's bits, or false (the caller
+  // forms it on the host) for a shape or a series the kernel leaves to the host, a stalled grid,
+  // or PICARD_DEVICE_EXPM=0. Tags of the grid barrier continue from the last call (xm_seq_).
+  const bool device_expm_ = !(std::getenv("PICARD_DEVICE_EXPM") && std::atoi(std::getenv("PICARD_DEVICE_EXPM")) == 0);
+  unsigned long long xm_seq_ = 0;
+  size_t xm_n_ = 0;
+  // below this n the host's products are faster than the kernel's latency-bound steps (measured:
+  // n = 64 host 0.05 ms, device 0.12–0.14 ms); PICARD_DEVICE_EXPM_MIN_N overrides (the tests: 32)
+  size_t xm_min_n_ = std::getenv("PICARD_DEVICE_EXPM_MIN_N") ? (size_t)std::atoi(std::getenv("PICARD_DEVICE_EXPM_MIN_N")) : 96;
+  double* d_xm = nullptr; size_t cap_xm = 0;
+  PinSlot pin_xm_, pin_xmo_{nullptr, 0, nullptr, false, hipHostMallocCoherent};
+  uint64_t n_device_expm_ = 0;
+  bool device_matrix_exp(const double* a, size_t n, double* out) override {
+    if (!device_expm_ || n < xm_min_n_ || n > (size_t)XM_MAXN || n % 32 != 0) return false;
+    HIP_OK(hipSetDevice(device));
+    const size_t nn = n * n, G = (n / 32) * (n / 32);
+    // device: [A | work: P1…P4, R0, R1 | granules: 2·3·G {value, tag}]; E and the status word are
+    // stored by the kernel straight into coherent pinned host memory (no D2H copy on the timeline)
+    const size_t off_w = nn, off_g = 7 * nn, total = off_g + 2 * 3 * G * 2;
+    const size_t cap0 = cap_xm;
+    double* base = ensure(d_xm, cap_xm, total);
+    // a new buffer (or a new n: the granules moved) starts with tag 0 everywhere, below any seq0
+    if (cap_xm != cap0 || n != xm_n_) HIP_OK(hipMemsetAsync(base + off_g, 0, 2 * 3 * G * 2 * sizeof(double), stream));
+    xm_n_ = n;
+    double* h = (double*)pin_acquire(pin_xm_, nn * sizeof(double));
+    std::memcpy(h, a, nn * sizeof(double));
+    HIP_OK(hipMemcpyAsync(base, h, nn * sizeof(double), hipMemcpyHostToDevice, stream));
+    pin_release(pin_xm_);
+    double* o = (double*)pin_acquire(pin_xmo_, (nn + 1) * sizeof(double));
+    lds_attr((const void*)k_expm_ps, XM_LDS);
+    const unsigned long long seq0 = xm_seq_ + 1;
+    xm_seq_ += 128;  // more than the barriers of one call (≤ 65)
+    HIP_OK(hipEventRecord(ev[1], stream));
+    k_expm_ps<<<(unsigned)(8 * G), XM_THREADS, XM_LDS, stream>>>(base, (int)n, base + off_w, o, (int*)(o + nn),
+                                                                 base + off_g, seq0, 1u << 20);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev[2], stream));
+    pin_release(pin_xmo_);
+    sync();
+    int st = 0;
+    std::memcpy(&st, o + nn, sizeof(int));
+    if (std::getenv("PICARD_TRACE_EXPM")) {
+      float km = 0.f;
+      HIP_OK(hipEventElapsedTime(&km, ev[1], ev[2]));
+      std::fprintf(stderr, "[picard-expm] n %zu kernel %.3f ms status %d\n", n, km, st);
+    }
+    if (st != 0) {
+      if (std::getenv("PICARD_TRACE"))
+        std::fprintf(stderr, "[picard-expm] n %zu: device map declined (status %d: 1 = the host's series, 2 = stalled grid)\n", n, st);
+      return false;
+    }
+    std::memcpy(out, o, nn * sizeof(double));
+    ++n_device_expm_;
+    return true;
+  }
   double* d_jade = nullptr; size_t cap_jade = 0;  // the JADE sweeps' buffer (jade_sweeps_impl)
 
   void moments4(const double* w, size_t nc, const double* mu, double* out) override {

@@ -146,6 +146,13 @@ class Evaluator {
     (void)w; (void)z; (void)nc; (void)mu; (void)d; (void)alphas; (void)na; (void)ll_out; (void)bnd_out;
     return false;
   }
+  // expm(a) for an n × n a (math.rs:38-74) with the bits of the host's matrix_exp, formed where
+  // the evaluator's passes run (try 1's map of an orthogonal search); false = not here (the
+  // caller forms it on the host)
+  virtual bool device_matrix_exp(const double* a, size_t n, double* out) {
+    (void)a; (void)n; (void)out;
+    return false;
+  }
   // JADE sweeps (jade.rs:37-69) on the np = n(n+1)/2 cumulant matrices A, packed
   // position-major (A[pos(k,l)·np + m], k ≤ l, pos as in jade_warm_start). On
   // success v (n×n, row-major) holds the accumulated rotation V and *log the

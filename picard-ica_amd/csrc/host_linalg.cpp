@@ -1,5 +1,6 @@
 // Host N×N linear algebra; see host_linalg.hpp.
 #include "host_linalg.hpp"
+#include "expm_plan.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -461,7 +462,8 @@ Mat matrix_exp(const Mat& a) {
   const size_t n = a.rows;
   const double norm = max_abs(a);
   if (norm < 1e-15) return Mat::eye(n);
-  const int s = (int)std::fmax(std::ceil(std::log2(norm)), 0.0);
+  // s = max(⌈log2 ‖A‖max⌉, 0), exactly (expm_plan.hpp: the device map k_expm_ps makes the same choice)
+  const int s = std::max(pc_ceil_log2(norm), 0);
   const double sc = std::ldexp(1.0, s);
   Mat as = a;
   for (double& v : as.a) v /= sc;
@@ -478,6 +480,7 @@ Mat matrix_exp(const Mat& a) {
   //   remainder bound is below 1e-17, (t, m) minimising ⌊m/4⌋ + t products: a Horner recursion
   //   in B^4 over blocks Σ_{i<4} B^i/(4j+i)!, then s + t squarings. The powers of two 2^-it are
   //   folded into the block coefficients and the Horner step (exact).
+  //   The plan (t, m) is expm_plan (expm_plan.hpp), shared with the device.
   std::vector<Mat> pw(5);
   pw[1] = as;
   double nu[5] = {1.0, norm_inf(as), 0.0, 0.0, 0.0};
@@ -485,36 +488,9 @@ Mat matrix_exp(const Mat& a) {
     pw[k] = matmul(pw[k - 1], as);
     nu[k] = norm_inf(pw[k]);
   }
-  // tails[t][m] = Σ_{k>m} bound(k)/k! at scale 2^-t (terms beyond k = 90 are negligible here)
-  constexpr int KMAX = 90, TMAX = 6;
-  double tails[TMAX + 1][32];
-  for (int t = 0; t <= TMAX; ++t) {
-    const double f = std::ldexp(1.0, -t);
-    const double fr[4] = {1.0, f, f * f, f * f * f};
-    const double b4 = nu[4] * fr[2] * fr[2];
-    double term[KMAX + 1] = {};
-    double inv_fact = 1.0, p4 = 1.0;
-    for (int k = 1; k <= KMAX; ++k) {
-      inv_fact /= (double)k;
-      if (k % 4 == 0) p4 *= b4;
-      term[k] = p4 * nu[k % 4] * fr[k % 4] * inv_fact;
-      if (k % 4 == 3 && p4 * inv_fact < 1e-250) break;  // the rest is negligible (and no subnormals)
-    }
-    double sum = 0.0;
-    for (int k = KMAX; k > 31; --k) sum += term[k];
-    for (int m = 31; m >= 0; --m) {
-      tails[t][m] = sum;
-      if (m > 0) sum += term[m];
-    }
-  }
-  if (std::isfinite(nu[4]) && tails[0][30] < 1e-17) {
-    int t = 0, m = 30, best_cost = 1 << 30;
-    for (int tt = 0; tt <= TMAX; ++tt)
-      for (int mm = 1; mm <= 30; ++mm)
-        if (tails[tt][mm] < 1e-17) {
-          if (mm / 4 + tt < best_cost) best_cost = mm / 4 + tt, t = tt, m = mm;
-          break;
-        }
+  const ExpmPlan plan = expm_plan(nu);
+  if (plan.converged) {
+    const int t = plan.t, m = plan.m;
     // B̃ = 2^-t·B: B̃^(4j+i) = (f4·B^4)^j·f^i·B^i, so R_nb = block_nb and R_j = R_(j+1)·(f4·B^4) +
     // block_j with block_j = Σ_{i<4, 4j+i ≤ m} f^i/(4j+i)!·B^i (B^0 = I)
     const double f = std::ldexp(1.0, -t), f4 = std::ldexp(1.0, -4 * t);

@@ -581,8 +581,13 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           }
           ahead_->submit(direction, W_, tries);
         }
+        // try 1's map is on the critical path: expm(α·D) where the passes run when the evaluator
+        // can (DeviceCtx: k_expm_ps, the host's bits), else on the host
         const double tm = now_ms();
-        r.w = matmul(matrix_exp(scale(direction, alpha)), W_);
+        const Mat da = scale(direction, alpha);
+        Mat e(n, n);
+        if (!ev_->device_matrix_exp(da.data(), n, e.data())) e = matrix_exp(da);
+        r.w = matmul(e, W_);
         map1_ms_ = now_ms() - tm;
       } else {
         r.w = ahead_->get(k, &ahead_wait_ms_);

@@ -159,14 +159,15 @@ def test_g8_non_finite_falls_back(pa, rng):
     assert np.isnan(got["G"]).all() and np.isnan(got["ll"]).all()
 
 
-@pytest.mark.parametrize("scale,digit_g", [(2.0, True), (8.0, False), (1e5, False)])
+@pytest.mark.parametrize("scale,digit_g", [(1.5, True), (16.0, False), (1e5, False)])
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("exp", 1.0)])
-def test_g8_outlying_samples(pa, po, rng, scale, digit_g, dens):
+def test_g8_outlying_samples(pa, po, scale, digit_g, dens):
     """A few samples far above the typical one: y's fixed point is set by the
     largest sample exponent, so its G error grows with the spread Δe between that exponent and
-    the typical one (this mixture: Δe ≈ 0.8 clean, ≈ 1.8 / 3.8 / 10.7 with three samples 2× /
-    8× / 1e5× the rest; the digit G stage measured 1.1e-12 at Δe = 3.8). The stage keeps only
-    Δe ≤ 3 at this T (DeviceCtx::g8_spread_ok); G is within 1e-12 of the oracle either way."""
+    the typical one (this mixture: Δe ≈ 0.8 clean; three samples 1.5× / 16× / 1e5× the rest add
+    ≈ 0.6 / 4 / 17 bits; the digit G stage measured 1.1e-12 at Δe ≈ 3.8). The stage keeps only
+    Δe ≤ 2.5 at this T (DeviceCtx::g8_spread_ok); G is within 1e-12 of the oracle either way."""
+    rng = np.random.default_rng(8643)  # its own data: the spread is a property of the sample
     n, t = 128, 5003
     x = laplace_mix(rng, n, t)
     x[:, [17, 2500, 4999]] *= scale

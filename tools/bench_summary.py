@@ -10,9 +10,8 @@ if d.get("whole_fit"):
     print("whole fit %.4g samples/s/iter  %.2f s  %.2f passes/iter" % (w["samples_per_s_per_iter"], w["iterations_s"],
                                                                      w["passes_per_iter"]))
 for r in d.get("roofline_kernels", []):
-    print("  %-44s %8.2f ms  %.3f of peak %.1f (%.3f of fp64 MFMA)  traffic %s" % (
-        r["kernel"], r["avg_kernel_ms"], r.get("frac_of_executed_mix_peak", r["frac"]), r.get("executed_mix_peak_tflops", r["peak"]),
-        r.get("frac_of_fp64_mfma_peak", r["frac"]), r["traffic"]))
+    print("  %-44s %8.2f ms  frac %.3f (%s %.4g of %.4g)  traffic %s" % (
+        r["kernel"], r["avg_kernel_ms"], r["frac"], r["unit"], r["achieved"], r["peak"], r["traffic"]))
 for k, c in (d.get("other_configs") or {}).items():
     print("  %s %-48s iters %4d  setup %.2fs  iter %.2fs  %.3g samples/s/iter  passes %d  amari %.2e" % (
         k, c["workload"], c["iters_to_tol"], c["setup_s"], c["iterations_s"], c["samples_per_s_per_iter"],
@@ -25,5 +24,5 @@ if d.get("cpu_baseline"):
     print("  C3 cpu_baseline %.4g %s (%s cores)" % (d["cpu_baseline"]["value"], d["cpu_baseline"]["unit"], d["cpu_baseline"]["cores"]))
 if d.get("transform"):
     t = d["transform"]
-    print("  transform %s %.2f ms  %.1f TF/s (%.3f of MFMA peak)  %.0f GB/s  bound %.2f ms" % (
-        t["kernel"], t["avg_kernel_ms"], t["achieved_tflops"], t["frac_mfma"], t["hbm_gbs_algorithmic"], t["bound_ms"]))
+    print("  transform %s %.2f ms  frac %.3f of its executed roof (%.2f ms)  %.0f GB/s" % (
+        t["kernel"], t["avg_kernel_ms"], t["frac"], t["executed_bound_ms"], t["hbm_gbs_algorithmic"]))
