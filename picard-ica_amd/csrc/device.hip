@@ -2005,7 +2005,7 @@ k_multi_loss2_oz(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc
 // host passes k_multi_loss2_oz's sample partition (nwgx, bpw), and each lane sums its samples
 // in that kernel's order, so the per-workgroup partials — and every decision — are bit for bit
 // the same. NT = the tries' accumulators held (10: ls_tries = 10 fits without spilling at KSO = 4).
-template <int KSO, int DENS, bool NEED_Q, int NT>
+template <int KSO, int DENS, bool NEED_Q, int NT, bool FENCE = true>
 __global__ void __launch_bounds__(FUSED_THREADS, 1)
 k_multi_loss2_ozy(const uint8_t* __restrict__ xsl, const double* __restrict__ xsc, const uint8_t* __restrict__ wsl_g,
                   const double* __restrict__ wsc, int ncp, double alpha, const double* __restrict__ alphas, int na,
@@ -2081,7 +2081,9 @@ k_multi_loss2_ozy(const uint8_t* __restrict__ xsl, const double* __restrict__ xs
             d4 yj;
 #pragma unroll
             for (int r = 0; r < 4; ++r) yj[r] = __builtin_fma(aj, zv[r], yv[r]);
-            loss_acc4<DENS, NEED_Q, 1>(yj, alpha, m2a, s_exp_tab, racc[u]);
+            // FENCE = false: the tries' density chains may interleave (each try's sums keep their
+            // element order, so the same bits)
+            loss_acc4<DENS, NEED_Q, 1, FENCE>(yj, alpha, m2a, s_exp_tab, racc[u]);
             if ((b & (RENORM_BLOCKS - 1)) == RENORM_BLOCKS - 1) acc_renorm<DENS>(racc[u]);
           }
         }
@@ -3296,6 +3298,8 @@ struct DeviceCtx : Evaluator {
     const size_t lds = (size_t)2 * (oz_block_bytes<KSO>() + 256);
     auto k = na <= 10 ? (want_y2 ? k_multi_loss2_ozy<KSO, D, true, 10> : k_multi_loss2_ozy<KSO, D, false, 10>)
                       : (want_y2 ? k_multi_loss2_ozy<KSO, D, true, ML_NA> : k_multi_loss2_ozy<KSO, D, false, ML_NA>);
+    if (!multi_fence_ && na <= 10)  // (A/B knob PICARD_MULTI_FENCE=0: unfenced try chains)
+      k = want_y2 ? k_multi_loss2_ozy<KSO, D, true, 10, false> : k_multi_loss2_ozy<KSO, D, false, 10, false>;
     lds_attr((const void*)k, (int)lds);
     k<<<xcd_grid(nwg, nroles), FUSED_THREADS, lds, stream>>>(d_xsl, d_xsc, d_wsl, d_wsc, ncp, alpha, dal, na, ybuf_read_,
                                                              bpw, n_blocks, part, (uint64_t)nwg);
@@ -3606,6 +3610,7 @@ struct DeviceCtx : Evaluator {
   uint64_t n_multi_ybuf_ = 0;
   const double* ybuf_read_ = nullptr;  // the slot the current multi-try pass reads
   const bool multi_ybuf_ = !(std::getenv("PICARD_MULTI_YBUF") && std::atoi(std::getenv("PICARD_MULTI_YBUF")) == 0);
+  const bool multi_fence_ = !(std::getenv("PICARD_MULTI_FENCE") && std::atoi(std::getenv("PICARD_MULTI_FENCE")) == 0);
   const int gram_sbb_ = std::getenv("PICARD_GRAM_SBB") && std::atoi(std::getenv("PICARD_GRAM_SBB")) == 1 ? 1 : 2;
   double* d_slab = nullptr; size_t cap_slab = 0;
   double* d_trow = nullptr; size_t cap_trow = 0;
