@@ -253,6 +253,7 @@ Solver::Solver(Evaluator* ev, const pc_config& cfg) : ev_(ev), cfg_(cfg) {
   trace_ = std::getenv("PICARD_TRACE") != nullptr;
   keep_y_ = std::getenv("PICARD_KEEP_Y") != nullptr;
   no_multi_ = std::getenv("PICARD_NO_MULTI") != nullptr;
+  if (const char* e = std::getenv("PICARD_CVX")) cvx_on_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("PICARD_MULTI_GROUP")) multi_group_ = (size_t)std::max(0, std::atoi(e));
   split_first_ = std::getenv("PICARD_SPLIT_FIRST") != nullptr;
   init_core();
@@ -440,6 +441,76 @@ double Solver::curvature_lower_bound(double alpha) const {
          0.5 * ls_curv_ * r * r;
 }
 
+// Convexity rejection (schedule only, no decision changes), non-orthogonal searches with the
+// tanh density and every s_i = +1 (not extended). Along the try path W(α) = (I + αD)·W
+// (core.rs:121) the sources y_t(α) = y_t + α·D·y_t are affine in α, so the density part of the
+// loss (core.rs:39-85), f(α) = Σ_i Σ_t ℓ(y_it(α))/T with ℓ″ = a·(1 − tanh²(a·y)) ≥ 0, is convex:
+//   f(α) ≥ f(0) + α·f′(0),  f′(0) = Σ_ij D_ij·G_ij/T  (G = ψ·Yᵀ of the current W's pass).
+// The log-determinant part is −log|det W| − log|det(I + αD)|, and Hadamard's inequality gives
+// log|det(I + αD)| ≤ Σ_k ½·log‖e_k + α·D_k‖² (D_k: row k). So
+//   L(α) − L(0) ≥ B(α) = α·f′(0) − Σ_k ½·log((1 + α·D_kk)² + α²·Σ_{j≠k} D_kj²),
+// which is α·⟨g, D⟩ − O(α²) with ⟨g, D⟩ = f′(0) − tr D the search's slope: positive at small α
+// along a non-descent direction (a third of C4's failed searches). Where B(α) exceeds the
+// rounding of both computed losses (the pass's G entries to 1e-10 of Σ_t|ψ_i·y_j| ≤ T·√(Σy_j²/T)
+// as |ψ| ≤ 1; the density sums to 1e-9 of Σ|ℓ| with |ℓ(y)| ≤ |y| + ln2/a; each log|det| to 1e-9
+// per row — all far above the kernels' and the LU's actual rounding), the exact pass at α would
+// reject the try (core.rs:127-140). Returns how many leading tries (α = 1, ½, …) remain once the
+// trailing tries that the bound rejects are dropped; tries between the first and the last
+// rejection still run. When none remains, the search fails without a pass, as it would with
+// every pass run (its result is then discarded for the gradient fallback, core.rs:349-364).
+size_t Solver::convexity_trim(const Mat& d, size_t tries, double* b_first) const {
+  const size_t n = nc_;
+  *b_first = 0.0;
+  if (!cvx_on_ || cfg_.ortho || extended_ || cfg_.density.kind != PC_DENSITY_TANH || !(cfg_.density.alpha > 0.0) ||
+      tries == 0)
+    return tries;
+  for (size_t i = 0; i < n; ++i)
+    if (signs_[i] != 1.0) return tries;
+  const double t = (double)T_, a = cfg_.density.alpha;
+  const double* g = S_.G();
+  const double* y2 = S_.y2();
+  std::vector<double> ry(n), dkk(n), off(n);
+  double sry = 0.0;
+  for (size_t j = 0; j < n; ++j) {
+    const double q = y2[j] / t;
+    if (!(q > 0.0) || !std::isfinite(q)) return tries;  // Σy² not computed by this pass
+    ry[j] = std::sqrt(q);
+    sry += ry[j];
+  }
+  double fp = 0.0, dabs = 0.0;  // f′(0); Σ_ij |D_ij|·√(Σy_j²/T) ≥ Σ_i E|(D·y)_i|
+  for (size_t i = 0; i < n; ++i) {
+    double o = 0.0;
+    for (size_t j = 0; j < n; ++j) {
+      const double v = d(i, j);
+      fp += v * (g[i * n + j] / t);
+      dabs += std::fabs(v) * ry[j];
+      if (j != i) o += v * v;
+    }
+    dkk[i] = d(i, i);
+    off[i] = o;
+  }
+  if (!std::isfinite(fp) || !std::isfinite(dabs)) return tries;
+  auto bound = [&](double al) {
+    double h = 0.0;  // Σ_k ½·log‖e_k + α·D_k‖², each row's square sum a sum of non-negative terms
+    for (size_t k = 0; k < n; ++k) {
+      const double u = 1.0 + al * dkk[k];
+      h += 0.5 * std::log((u * u + al * al * off[k]) * (1.0 + 1e-12));
+    }
+    const double slack = al * 1e-10 * dabs + 2e-9 * (sry + al * dabs + (double)n * 0.6931471805599453 / a) +
+                         2e-9 * (double)n + 1e-12;
+    return al * fp - h - slack;  // −inf row terms (a zero row of I + αD: W(α) singular) reject
+  };
+  size_t keep = tries;
+  double al = std::ldexp(1.0, -(int)(tries - 1));
+  double b = 0.0;
+  while (keep > 0 && (b = bound(al)) > 0.0) {
+    *b_first = b;
+    --keep;
+    al *= 2.0;
+  }
+  return keep;
+}
+
 // Orthogonal line search, host side: W_k = expm(α_k·D)·W (core.rs:118-125) for
 // α_k = 2^-k. Try 0's map is on the critical path; a helper thread forms the
 // maps of tries 1, 2, … while the device evaluates the earlier tries, so the
@@ -561,6 +632,17 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
   const bool ortho = cfg_.ortho != 0;
   double alpha = 1.0;
   LsResult r{false, W_, S_, current_loss_, Mat(), false, 0, false, false};
+  if (!ortho && !full_first) {  // the trailing tries the convexity bound rejects run no pass
+    double b = 0.0;
+    const size_t keep = convexity_trim(direction, tries, &b);
+    if (keep < tries) {
+      cvx_skips_ += tries - keep;
+      if (trace_)
+        std::fprintf(stderr, "[picard-cvx] tries %zu-%zu rejected by the convexity bound (at alpha %.3e: %.3e)\n",
+                     keep + 1, tries, std::ldexp(1.0, -(int)keep), b);
+      tries = keep;
+    }
+  }
   // a paired screen's second try (Evaluator::eval_loss_screen2): its rows, for try pair_k
   std::vector<double> pair_ll, pair_bnd;
   size_t pair_k = tries;
@@ -1068,11 +1150,11 @@ bool Solver::step() {
                  t_grad - step_t0, t_dir - t_grad, t_curv - t_dir, ls_host);
     std::fprintf(stderr, "[picard-trace] iter %zu gnorm %.3e first_ls_tries %zu ok %d fallback %d fb_tries %zu partial %d slope %.3e"
                  " step_ms %.3f eval_ms %.3f host_ms %.3f map1_ms %.3f map_wait_ms %.3f screens %llu rejected %llu"
-                 " curv_skips %llu screen_pairs %llu\n",
+                 " curv_skips %llu screen_pairs %llu cvx_skips %llu\n",
                  iter_ + 1, gradient_norm_, first_tries, first_ok ? 1 : 0, first_ok ? 0 : 1, first_ok ? 0 : res.tries,
                  res.partial ? 1 : 0, slope, step_ms, dev_ms, step_ms - dev_ms, map1_ms_, ahead_wait_ms_ - wait_t0,
                  (unsigned long long)screen_passes_, (unsigned long long)screen_rejects_,
-                 (unsigned long long)curv_skips_, (unsigned long long)screen_pairs_);
+                 (unsigned long long)curv_skips_, (unsigned long long)screen_pairs_, (unsigned long long)cvx_skips_);
   }
   prev_step_ = std::move(res.step);
   has_prev_step_ = true;

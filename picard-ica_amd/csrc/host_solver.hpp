@@ -131,6 +131,12 @@ class Solver {
   Mat C1_;
   double ls_slope_ = 0.0, ls_curv_ = 0.0, ls_q_ = 0.0, ls_k3_ = 0.0, ls_slack_ = 0.0;
   uint64_t curv_skips_ = 0;
+  // Convexity rejection of non-orthogonal tanh tries (Solver::convexity_trim): the trailing
+  // tries of a search whose lower bound exceeds the losses' rounding run no pass
+  // (PICARD_CVX=0 turns it off); cvx_skips_ counts them
+  bool cvx_on_ = true;
+  uint64_t cvx_skips_ = 0;
+  size_t convexity_trim(const Mat& d, size_t tries, double* b_first) const;
   // non-orthogonal searches: tries in the first multi-try pass (0: all; PICARD_MULTI_GROUP)
   // and how many searches needed a second pass for the rest
   size_t multi_group_ = 0;

@@ -303,3 +303,80 @@ def test_staged_multi_try_decisions_unchanged(pa, po, dg, group, monkeypatch):
     assert any(n == group for n in c1)  # first passes capped at `group` tries
     assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
     assert np.array_equal(r1.unmixing, r0.unmixing)
+
+
+@pytest.mark.parametrize("a,aniso", [(1.0, False), (0.5, False), (2.0, False), (1.0, True)])
+def test_convexity_bound_holds(a, aniso):
+    """The bound behind the non-orthogonal convexity rejection (Solver::convexity_trim): along
+    W(α) = (I + αD)·W the tanh loss L(α) = −log|det W(α)| + Σ_i mean_t ℓ(y_it(α)) satisfies
+    L(α) − L(0) ≥ α·Σ_ij D_ij·G_ij/T − Σ_k ½·log((1 + α·D_kk)² + α²·Σ_{j≠k} D_kj²) with
+    G = ψ(Y)·Yᵀ (convexity of ℓ along the affine y(α), Hadamard's inequality for the determinant),
+    for general D (descent and non-descent, small and large) and W."""
+    rng = np.random.default_rng(11)
+    n, t = 8, 4000
+    x = rng.laplace(size=(n, t))
+    x -= x.mean(axis=1, keepdims=True)
+    ev, u = np.linalg.eigh(x @ x.T / t)
+    x = (u / np.sqrt(ev)).T @ x
+    if aniso:
+        x = np.geomspace(0.25, 4.0, n)[:, None] * x
+
+    def ell(y):  # density.rs Tanh log_lik
+        return np.abs(y) + np.log1p(np.exp(-2 * a * np.abs(y))) / a
+
+    def loss(wm):
+        return -np.linalg.slogdet(wm)[1] + float(np.sum(ell(wm @ x).mean(axis=1)))
+
+    hits = 0
+    for _ in range(30):
+        w = rng.normal(size=(n, n)) + 2 * np.eye(n)
+        y = w @ x
+        g = np.tanh(a * y) @ y.T / t
+        d = rng.normal(size=(n, n)) * rng.uniform(0.01, 2.0)
+        fp = float(np.sum(d * g))
+        off = np.sum(d * d, axis=1) - np.diag(d) ** 2
+        for alpha in 2.0 ** -np.arange(0, 10):
+            h = 0.5 * np.sum(np.log((1 + alpha * np.diag(d)) ** 2 + alpha * alpha * off))
+            bound = alpha * fp - h
+            lhs = loss((np.eye(n) + alpha * d) @ w) - loss(w)
+            assert lhs >= bound - 1e-12 * (1 + abs(lhs)), (alpha, lhs, bound)
+            hits += bound > 0
+    assert hits > 0  # the bound does reject tries in this sample
+
+
+def test_convexity_rejection_decisions_unchanged(pa, po, dg, capfd, monkeypatch):
+    """Non-orthogonal tries rejected by the convexity bound (Solver::convexity_trim) run no pass
+    and change no decision: on the bench mixture some L-BFGS directions do not descend, their
+    trailing tries (all of them, for some searches) are dropped, and the fit is bit-identical to
+    the one with every try evaluated (PICARD_CVX=0)."""
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    x, _ = dg.generate_data(12, 8000, 42)[:2]
+    calls = []
+
+    def ev(w, mu, d, need_h):
+        return po.pass_stats(w, mu, x, density_of(po, d), need_h)
+
+    def multi(w, z, alphas, mu, d):
+        calls.append(len(alphas))
+        ll, y2 = [], []
+        for al in alphas:
+            st = po.pass_stats(w + al * z, mu, x, density_of(po, d), False)
+            ll.append(st["ll"])
+            y2.append(st["y2"])
+        return np.array(ll), np.array(y2)
+
+    def fit(cvx):
+        monkeypatch.setenv("PICARD_CVX", "1" if cvx else "0")
+        calls.clear()
+        r = pa.fit_with_host_evaluator(
+            x.shape[0], x.shape[1], pa.PicardConfig(ortho=False, extended=False, random_state=7, max_iter=80),
+            rowsum=lambda: x.sum(axis=1), gram=lambda mu: (x - mu[:, None]) @ (x - mu[:, None]).T,
+            eval=ev, sources=lambda w, mu: w @ (x - mu[:, None]), eval_loss_multi=multi)
+        return r, sum(calls), capfd.readouterr().err
+
+    r0, t0, e0 = fit(False)
+    r1, t1, e1 = fit(True)
+    assert "[picard-cvx]" not in e0 and "[picard-cvx]" in e1
+    assert t1 < t0  # fewer tries evaluated
+    assert r1.n_iterations == r0.n_iterations and r1.converged == r0.converged
+    assert np.array_equal(r1.unmixing, r0.unmixing)
