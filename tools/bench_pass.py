@@ -1,5 +1,6 @@
 """Time the fused evaluation pass alone (HIP events around the kernel).
-Usage: python tools/bench_pass.py N T [density] [reps] [need_h]"""
+Usage: python tools/bench_pass.py N T [density] [reps] [need_h] [need_y2]  (need_y2=0: the orthogonal
+solver's pass, no Σy²)"""
 import sys
 import os
 import time
@@ -11,16 +12,17 @@ n = int(sys.argv[1]); t = int(float(sys.argv[2]))
 dens = sys.argv[3] if len(sys.argv) > 3 else "tanh"
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 need_h = bool(int(sys.argv[5])) if len(sys.argv) > 5 else False
+need_y2 = bool(int(sys.argv[6])) if len(sys.argv) > 6 else True
 d = {"tanh": pa.DensityType.tanh(), "exp": pa.DensityType.exp(), "cube": pa.DensityType.cube()}[dens]
 ctx = pa.DeviceContext(0)
 ctx.generate(n, t, 42)
 mu = ctx.rowsum() / t
 w = np.linalg.qr(np.random.default_rng(0).normal(size=(n, n)))[0] * 0.05
-ctx.eval(w, mu, d, need_h)
+ctx.eval(w, mu, d, need_h, need_y2)
 ctx.kernel_stats(reset=True)
 t0 = time.perf_counter()
 for _ in range(reps):
-    ctx.eval(w, mu, d, need_h)
+    ctx.eval(w, mu, d, need_h, need_y2)
 wall = (time.perf_counter() - t0) / reps
 k, c, nl = ctx.kernel_stats()
 avg = k / nl if nl else c / max(reps, 1)  # tiled / generic paths: whole eval call
