@@ -209,3 +209,28 @@ def test_g8_fit_matches_f64_g_fit(pa, rng):
     assert r8.converged and r64.converged
     assert abs(r8.n_iterations - r64.n_iterations) <= 2
     assert np.max(np.abs(r8.unmixing - r64.unmixing)) <= 1e-6
+
+
+@pytest.mark.parametrize("n,t", [(96, 20000), (128, 12000)])
+def test_g8_fit_vs_oracle(pa, po, dg, n, t):
+    """A whole Picard-O fit on the shipped arithmetic at 64 < N ≤ 128 — int8 Y, the digit G stage,
+    screens, the device try-1 map (N ≥ 96) — against the numpy oracle's fp64 fit (the
+    C2 golden fit is N = 64 and never runs the digit G stage): both converge, iterations ±2,
+    |ΔAmari| to the generated mixing ≤ 1e-6 (north_star's tolerance), unmixing within 1e-5."""
+    x, _, a = dg.generate_data(n, t, 42)
+    ctx = pa.DeviceContext(0)
+    ctx.load(x)
+    sv = pa.Solver(ctx, pa.PicardConfig(w_init=np.eye(n), max_iter=200, want_sources=False))
+    while not sv.step():
+        pass
+    r = sv.finish()
+    g8 = ctx.g8_passes
+    sv.close()
+    ctx.close()
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(n), max_iter=200))
+    assert g8 > 0  # the digit G stage ran
+    assert r.converged and ro.converged
+    assert abs(r.n_iterations - ro.n_iterations) <= 2, (r.n_iterations, ro.n_iterations)
+    am, amo = pa.utils.amari_distance(r.full_unmixing(), a), po.amari_distance(ro.full_unmixing(), a)
+    assert abs(am - amo) <= 1e-6, (am, amo)
+    assert np.max(np.abs(r.full_unmixing() - ro.full_unmixing())) <= 1e-5 * np.max(np.abs(ro.full_unmixing()))
