@@ -211,8 +211,8 @@ def test_g8_fit_matches_f64_g_fit(pa, rng):
     assert np.max(np.abs(r8.unmixing - r64.unmixing)) <= 1e-6
 
 
-@pytest.mark.parametrize("n,t", [(96, 20000), (128, 12000)])
-def test_g8_fit_vs_oracle(pa, po, dg, n, t):
+@pytest.mark.parametrize("n,t,dens", [(96, 20000, "tanh"), (128, 12000, "tanh"), (96, 20000, "exp")])
+def test_g8_fit_vs_oracle(pa, po, dg, n, t, dens):
     """A whole Picard-O fit on the shipped arithmetic at 64 < N ≤ 128 — int8 Y, the digit G stage,
     screens, the device try-1 map (N ≥ 96) — against the numpy oracle's fp64 fit (the
     C2 golden fit is N = 64 and never runs the digit G stage): both converge, iterations ±2,
@@ -220,14 +220,15 @@ def test_g8_fit_vs_oracle(pa, po, dg, n, t):
     x, _, a = dg.generate_data(n, t, 42)
     ctx = pa.DeviceContext(0)
     ctx.load(x)
-    sv = pa.Solver(ctx, pa.PicardConfig(w_init=np.eye(n), max_iter=200, want_sources=False))
+    pd = pa.DensityType.tanh() if dens == "tanh" else pa.DensityType.exp()
+    sv = pa.Solver(ctx, pa.PicardConfig(w_init=np.eye(n), max_iter=200, want_sources=False, density=pd))
     while not sv.step():
         pass
     r = sv.finish()
     g8 = ctx.g8_passes
     sv.close()
     ctx.close()
-    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(n), max_iter=200))
+    ro = po.fit_with_config(x, po.PicardConfig(w_init=np.eye(n), max_iter=200, density=po.Density(dens, 1.0)))
     assert g8 > 0  # the digit G stage ran
     assert r.converged and ro.converged
     assert abs(r.n_iterations - ro.n_iterations) <= 2, (r.n_iterations, ro.n_iterations)
