@@ -210,8 +210,9 @@ int main() {
   // the bench mixture's shape at a size the callbacks finish in seconds: Laplace sources, a
   // random mixing
   Data d;
-  d.nf = 8;
-  d.t = 3000;
+  d.nf = std::getenv("PC_DRV_NF") ? (size_t)std::atoi(std::getenv("PC_DRV_NF")) : 8;  // (host-time probes)
+  d.t = std::getenv("PC_DRV_T") ? (size_t)std::atoi(std::getenv("PC_DRV_T")) : 3000;
+  const int only = std::getenv("PC_DRV_FIT") ? std::atoi(std::getenv("PC_DRV_FIT")) : -1;
   std::mt19937_64 rng(42);
   std::exponential_distribution<double> ex(1.0);
   std::bernoulli_distribution sg(0.5);
@@ -224,6 +225,7 @@ int main() {
     for (size_t k = 0; k < d.nf; ++k)
       for (size_t t = 0; t < d.t; ++t) d.x[i * d.t + t] += a[i * d.nf + k] * s[k * d.t + t];
   int bad = 0;
+  if (only == 0) return fit(d, 1, 1, PC_DENSITY_TANH, false, true, 0) != PC_OK;  // C3's kind alone
   bad += fit(d, 1, 1, PC_DENSITY_TANH, false, true, 0) != PC_OK;   // screened orthogonal (curvature)
   bad += fit(d, 1, 0, PC_DENSITY_TANH, false, false, 0) != PC_OK;  // every try exact
   bad += fit(d, 0, 0, PC_DENSITY_TANH, true, false, 0) != PC_OK;   // multi-try (convexity)
