@@ -47,8 +47,8 @@ HBM_PEAK_GBS = 8000.0
 I8_MFMA_PEAK_TOPS = 32768 / 16 * 1024 * 2.4e9 / 1e12   # = 5033
 OZ_PRODUCTS = 28   # digit products per multiply-add of the int8-digit Y stage (ozaki.inc)
 G8_PRODUCTS = 21   # … of the int8-digit G stage for tanh (fused_g8.inc: 6 + 6 digits, diagonals qa + qb >= 5)
-OZ_SCREEN_PRODUCTS = 10   # … of the line-search screen (diagonals D <= 3; an undecided try is
-                          # screened again on D <= 4, 15 products: counted at 10 here)
+OZ_SCREEN_PRODUCTS = 10   # … of a D <= 3 line-search screen; the screens' executed mix (6 products
+                          # at D <= 2, 10 at D <= 3, 15 at D <= 4) comes from pc_ctx_screen_products
 
 
 def parse():
@@ -325,6 +325,7 @@ def main():
     g8_timed = ctx.g8_passes - g8_before
     brk["screen"] = ctx.screen_stats(reset=False)
     screen_tries = ctx.screen_tries()  # a paired pass (two tries) counts 2
+    screen_products = ctx.screen_products()  # Σ digit products per try over those tries
 
     if dist is not None:
         import torch
@@ -401,7 +402,8 @@ def main():
                    "k_eval_fused_ws<tanh,noY2" + (",i8-digit Y>" if i8 else ">"))
     kinds = {"fused": ("k_eval_fused", fused_label, 4.0),
              "loss": ("k_eval_loss", "k_eval_loss_oz<tanh,nostore,noY2>" if i8 else "k_eval_loss2<tanh,nostore,noY2>", 2.0),
-             "screen": ("k_screen_oz", "k_screen_oz2<NB=8> (line-search screen: D<=3 digit products, fp32 l)", 2.0)}
+             "screen": ("k_screen_oz", "k_screen_oz2<NB=8> (line-search screen: D<=2 digit products, D<=3 where "
+                        "undecided, fp32 l)", 2.0)}
     rooflines = []
     for kind, (short, label, c) in kinds.items():
         ms, nl = brk.get(kind, (0.0, 0))
@@ -426,19 +428,24 @@ def main():
             peak, executed = FP64_MFMA_PEAK_TFLOPS, {"fp64_mfma_flops_per_launch": flops}
         if kind == "screen" and i8:
             # a truncated product (a bound, not a pass): priced only against what it executes —
-            # the D <= 3 digit products on the i8 matrix cores, per TRY
-            # (a paired pass screens two tries: twice the products of a single one)
+            # its digit products on the i8 matrix cores, per TRY (a paired
+            # pass screens two tries: twice the products of a single one); the mean over the
+            # executed mix of D <= 2 / 3 / 4 tries
             tries = max(screen_tries, nl)
             per_try_ms = ms / tries
-            executed = dict(executed, i8_ops_per_try=executed.pop("i8_ops_per_launch"))
+            executed.pop("i8_ops_per_launch")
+            prod_per_try = screen_products / tries if screen_products else OZ_SCREEN_PRODUCTS
+            executed = dict(executed, i8_ops_per_try=prod_per_try * 2.0 * n * n * t_local,
+                            digit_products_per_try=prod_per_try)
             tops = executed["i8_ops_per_try"] / (per_try_ms * 1e-3) / 1e12
             rooflines.append({"bound": "mfma", "achieved": tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
                               "frac": tops / I8_MFMA_PEAK_TOPS, "traffic": pmc.get(short, {}).get("hbm_bytes_per_launch"),
                               "kernel": label, "avg_kernel_ms": avg, "launches": nl, "tries": tries,
                               "ms_per_try": per_try_ms, "ms_per_step": ms / steps,
-                              "executed": executed, "note": "i8 digit products of diagonals D <= 3 per screened try "
-                              "against the i8 MFMA issue peak (launches: single and paired passes, avg_kernel_ms "
-                              "mixes both); the fp32 row terms (VALU) are not priced; traffic: a single pass"})
+                              "executed": executed, "note": "i8 digit products per screened try (the executed mix "
+                              "of D <= 2 and D <= 3 screens) against the i8 MFMA issue peak (launches: single and "
+                              "paired passes, avg_kernel_ms mixes both); the fp32 row terms (VALU) are not priced; "
+                              "traffic: a single pass of the form profiled in profiles/pmc_latest.json"})
             continue
         # `frac` is the binding executed roof: ideal time of what the kernel executes (its i8 / fp64
         # MFMA issue time, or the HBM time of its algorithmic bytes, whichever is larger) ÷ its

@@ -53,9 +53,10 @@ extern "C" {
  * operator boundary (they no longer abort a rank group). 5: pc_ctx_comm_timing,
  * pc_solver_timing, pc_solver_setup_timing, pc_ctx_alloc_stats, pc_last_teardown,
  * pc_device_mem_info. 6: pc_ctx_eval_loss_screen2 (paired screen), pc_ctx_screen_tries.
- * 7: pc_ctx_matrix_exp, pc_matrix_exp (no layout change).
+ * 7: pc_ctx_matrix_exp, pc_matrix_exp (no layout change). 8: pc_ctx_screen_digit_gram,
+ * pc_ctx_screen_products (no layout change).
  * pc_abi_version() returns the revision the library was built with. */
-#define PC_ABI_VERSION 7
+#define PC_ABI_VERSION 8
 
 /* src/error.rs:9-42 (NotConverged is reserved: the reference never returns it) */
 typedef enum {
@@ -410,7 +411,7 @@ int pc_ctx_eval_loss_screen(pc_ctx* ctx, const double* w, uint64_t nc, const dou
 /* Two tries' screens in ONE pass (w1, w2: nc × n_features each): ll1/bound1 and ll2/bound2 are
  * what pc_ctx_eval_loss_screen returns for w1 and for w2 alone (the same arithmetic per W; the
  * solver pairs the screened tries of a non-descent search with it). tanh, the
- * default D ≤ 3 fp32 screen only; PC_ERR_UNSUPPORTED where it does not apply (or with
+ * fp32 screen at D ≤ 2 or 3 only; PC_ERR_UNSUPPORTED where it does not apply (or with
  * PICARD_SCREEN_PAIRS=0). With a communicator, collective like pc_ctx_eval. */
 int pc_ctx_eval_loss_screen2(pc_ctx* ctx, const double* w1, const double* w2, uint64_t nc, const double* mu,
                              pc_density density, double* ll1, double* bound1, double* ll2, double* bound2,
@@ -419,6 +420,16 @@ int pc_ctx_eval_loss_screen2(pc_ctx* ctx, const double* w1, const double* w2, ui
 void pc_ctx_screen_stats(pc_ctx* ctx, double* kernel_ms, uint64_t* n_launches, int32_t reset);
 /* tries those passes covered since the same reset (a paired pass covers 2) */
 uint64_t pc_ctx_screen_tries(const pc_ctx* ctx);
+/* digit products those tries kept since the same reset, summed per try: (D+1)(D+2)/2 for a
+ * screen on diagonals D (6 for D ≤ 2, 10 for D ≤ 3, 15 for D ≤ 4) */
+uint64_t pc_ctx_screen_products(const pc_ctx* ctx);
+/* Inputs of the line-search screen's statistical bound for this context's shard (built on
+ * first use, with the int8 digit image): lam[b] (b < 7) ≥ the largest eigenvalue of the digit
+ * Gram D_b = Σ_t d_b,t·d_b,tᵀ (Gershgorin on the exact integer matrix), *s4 = Σ_t 4^(e_t) over
+ * the sample exponents (padding included). The screen's per-row tail is then
+ * 2^(f_i−12)·Σ_{dmax < a+b ≤ 6} 2^(−8(a+b))·√(s4·lam[b]·Σ_k w_a,ik²), or the worst-case tail
+ * where that is smaller. PC_ERR_UNSUPPORTED without an int8 digit image. */
+int pc_ctx_screen_digit_gram(pc_ctx* ctx, double* lam, double* s4, char* err, size_t errlen);
 /* Exhaustive accuracy of the fp32 instructions the line-search screen evaluates its
  * log-likelihood with (v_exp_f32, v_log_f32), measured on `device` against fp64 libm
  * over every fp32 input of the ranges the screen uses: out[0] max relative error of 2^z

@@ -211,6 +211,8 @@ def _load():
         "pc_ctx_eval_loss_screen": (C.c_int, [vp, d, u64, d, _Density, d, d, cp, sz]),
         "pc_ctx_eval_loss_screen2": (C.c_int, [vp, d, d, u64, d, _Density, d, d, d, d, cp, sz]),
         "pc_ctx_screen_tries": (u64, [vp]),
+        "pc_ctx_screen_digit_gram": (C.c_int, [vp, d, d, cp, sz]),
+        "pc_ctx_screen_products": (u64, [vp]),
         "pc_solver_create": (C.c_int, [vp, P(_Config), P(vp), cp, sz]),
         "pc_solver_step": (C.c_int, [vp, P(i32), cp, sz]),
         "pc_solver_finish": (C.c_int, [vp, P(_Result), cp, sz]),
@@ -238,7 +240,7 @@ EXPORTED = [
     "pc_ctx_release_caches",
     "pc_ctx_load", "pc_ctx_generate", "pc_ctx_download", "pc_ctx_n_local", "pc_ctx_t0",
     "pc_ctx_eval", "pc_ctx_eval_loss", "pc_ctx_eval_loss_multi", "pc_ctx_eval_loss_multi_bound", "pc_ctx_eval_complete", "pc_ctx_rowsum", "pc_ctx_gram", "pc_ctx_sources", "pc_ctx_sources_device", "pc_ctx_moments4",
-    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_set_g_stage", "pc_ctx_g8_passes", "pc_ctx_multi_ybuf_passes", "pc_ctx_matrix_exp", "pc_matrix_exp", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_ctx_screen_tries", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
+    "pc_ctx_jade", "pc_ctx_last_timing", "pc_ctx_kernel_stats", "pc_ctx_kernel_breakdown", "pc_ctx_set_y_stage", "pc_ctx_int8_passes", "pc_ctx_set_g_stage", "pc_ctx_g8_passes", "pc_ctx_multi_ybuf_passes", "pc_ctx_matrix_exp", "pc_matrix_exp", "pc_ctx_screen_stats", "pc_ctx_eval_loss_screen", "pc_ctx_eval_loss_screen2", "pc_ctx_screen_tries", "pc_ctx_screen_digit_gram", "pc_ctx_screen_products", "pc_device_synchronize", "pc_device_mem_info", "pc_device_check_fp32_transcendentals", "pc_solver_create", "pc_solver_step", "pc_solver_finish",
     "pc_solver_destroy", "pc_solver_last", "pc_solver_timing", "pc_solver_setup_timing", "pc_fit_with_evaluator",
 ]
 
@@ -799,6 +801,19 @@ class DeviceContext:
         """pc_ctx_screen_tries: tries the screen passes covered since the last screen_stats reset
         (a paired pass covers 2)."""
         return int(lib.pc_ctx_screen_tries(self.h))
+
+    def screen_products(self) -> int:
+        """pc_ctx_screen_products: digit products per try summed over the screened tries since the
+        last screen_stats reset (6 for a D ≤ 2 try, 10 for D ≤ 3, 15 for D ≤ 4)."""
+        return int(lib.pc_ctx_screen_products(self.h))
+
+    def screen_digit_gram(self):
+        """pc_ctx_screen_digit_gram: (lam[7], s4) — the largest-eigenvalue bounds of this shard's
+        digit Grams and Σ_t 4^e_t, the inputs of the screen's statistical bound."""
+        lam, s4 = np.zeros(7), C.c_double()
+        err = _errbuf()
+        _raise(lib.pc_ctx_screen_digit_gram(self.h, _ptr(lam), C.byref(s4), err, len(err)), err)
+        return lam, s4.value
 
     def screen_stats(self, reset: bool = False):
         """pc_ctx_screen_stats: (Σ screen-pass kernel ms, screen passes) since the last reset."""

@@ -44,6 +44,8 @@ uint64_t device_ctx_g8_passes(const Evaluator* e);
 uint64_t device_ctx_multi_ybuf_passes(const Evaluator* e);
 uint64_t device_ctx_int8_passes(const Evaluator* e);
 void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset);
+bool device_ctx_screen_digit_gram(Evaluator* e, double* lam, double* s4);
+uint64_t device_ctx_screen_products(const Evaluator* e);
 uint64_t device_ctx_screen_tries(const Evaluator* e);
 }  // namespace pcamd
 
@@ -548,6 +550,13 @@ void pc_ctx_screen_stats(pc_ctx* c, double* ms, uint64_t* n, int32_t reset) {
 }
 
 uint64_t pc_ctx_screen_tries(const pc_ctx* c) { return device_ctx_screen_tries(c->ev.get()); }
+uint64_t pc_ctx_screen_products(const pc_ctx* c) { return device_ctx_screen_products(c->ev.get()); }
+
+int pc_ctx_screen_digit_gram(pc_ctx* c, double* lam, double* s4, char* err, size_t errlen) {
+  return guarded_on(c->ev.get(), err, errlen, [&] {
+    if (!device_ctx_screen_digit_gram(c->ev.get(), lam, s4)) throw unsupported("no int8 digit image for this context");
+  });
+}
 
 int pc_device_check_fp32_transcendentals(int32_t device, double out[4]) {
   try {

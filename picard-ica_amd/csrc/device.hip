@@ -1177,25 +1177,27 @@ __device__ __forceinline__ double reduce_partials(const double* __restrict__ p, 
 }
 
 // min, max and a NaN flag of the n sample scales 2^e_t, per workgroup: out[3·b + {0, 1, 2}]
+// per workgroup: min, max, NaN flag and Σ v² of the sample scales v = 2^e_t (out[4·wg + c])
 __global__ void __launch_bounds__(256) k_xsc_range(const double* __restrict__ xsc, uint64_t n, double* __restrict__ out) {
-  __shared__ double s[3][256];
-  double lo = INFINITY, hi = 0.0, nan = 0.0;
+  __shared__ double s[4][256];
+  double lo = INFINITY, hi = 0.0, nan = 0.0, sq = 0.0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const double v = xsc[i];
     if (v != v) nan = 1.0;
-    else { lo = fmin(lo, v); hi = fmax(hi, v); }
+    else { lo = fmin(lo, v); hi = fmax(hi, v); sq = __builtin_fma(v, v, sq); }
   }
-  s[0][threadIdx.x] = lo; s[1][threadIdx.x] = hi; s[2][threadIdx.x] = nan;
+  s[0][threadIdx.x] = lo; s[1][threadIdx.x] = hi; s[2][threadIdx.x] = nan; s[3][threadIdx.x] = sq;
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
     if ((int)threadIdx.x < h) {
       s[0][threadIdx.x] = fmin(s[0][threadIdx.x], s[0][threadIdx.x + h]);
       s[1][threadIdx.x] = fmax(s[1][threadIdx.x], s[1][threadIdx.x + h]);
       s[2][threadIdx.x] = fmax(s[2][threadIdx.x], s[2][threadIdx.x + h]);
+      s[3][threadIdx.x] += s[3][threadIdx.x + h];
     }
     __syncthreads();
   }
-  if (threadIdx.x < 3) out[3 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
+  if (threadIdx.x < 4) out[4 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
 }
 
 // out[c·nc + row] = Σ_w partials[w·pstride + poff + c·ncp + row], c < nsets,
@@ -3900,7 +3902,7 @@ struct DeviceCtx : Evaluator {
     if (xsl_failed_ || nf > 256) return false;
     // the scratch of the Σ 2^e_t sum first: an allocation here may release the image
     const int nwg_e = (int)std::max<uint64_t>(1, std::min<uint64_t>((ldx + 4095) / 4096, 1024));
-    ensure(d_shift_part, cap_shift_part, std::max<size_t>((size_t)nwg_e + 1, 3 * (size_t)std::min(nwg_e, 256)));
+    ensure(d_shift_part, cap_shift_part, std::max<size_t>((size_t)nwg_e + 1, 4 * (size_t)std::min(nwg_e, 256)));
     if (xsl_failed_) return false;
     const uint64_t n_blocks = ldx / 16;
     const size_t need = (size_t)n_blocks * oz_bb();
@@ -3941,16 +3943,21 @@ struct DeviceCtx : Evaluator {
       const int nr = (int)std::min<uint64_t>(nwg, 256);
       k_xsc_range<<<nr, 256, 0, stream>>>(d_xsc, ldx, part);
       HIP_OK(hipGetLastError());
-      std::vector<double> mm(3 * (size_t)nr);
+      std::vector<double> mm(4 * (size_t)nr);
       HIP_OK(hipMemcpyAsync(mm.data(), part, mm.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
       sync();
-      double lo = INFINITY, hi = 0.0;
+      double lo = INFINITY, hi = 0.0, sq = 0.0;
       bool nan = false;
       for (int b = 0; b < nr; ++b) {
-        lo = std::min(lo, mm[3 * b]);
-        hi = std::max(hi, mm[3 * b + 1]);
-        nan |= mm[3 * b + 2] != 0.0;
+        lo = std::min(lo, mm[4 * b]);
+        hi = std::max(hi, mm[4 * b + 1]);
+        nan |= mm[4 * b + 2] != 0.0;
+        sq += mm[4 * b + 3];
       }
+      // Σ_t 4^e_t (padding included), an upper bound: each fp64 sum of positive terms errs by
+      // far less than 1e-9 relative (≤ 4096 sequential terms per thread, then trees)
+      xsc_s4_ = sq * (1.0 + 1e-9);
+      xg_valid_ = false;  // the digit Grams follow the image
       xsc_range_ok_ = !nan && lo > 0.0 && std::isfinite(hi);
       if (xsc_range_ok_) {
         (void)std::frexp(lo, &xsc_emin_);
@@ -3963,6 +3970,102 @@ struct DeviceCtx : Evaluator {
     return true;
   }
   double xsc_sum_ = 0.0;
+  // The line-search screen's statistical bound (screen_rank_bound): per digit plane b an upper
+  // bound λ_b on the largest eigenvalue of this shard's digit Gram D_b = Σ_t d_b,t·d_b,tᵀ
+  // (Gershgorin on the exact integer matrix), and S4 = Σ_t 4^e_t. Valid with the image.
+  double xsc_s4_ = 0.0;
+  double xg_lam_[OZ_SLICES] = {};
+  bool xg_valid_ = false, xg_failed_ = false;
+  uint64_t n_digit_gram_ = 0;
+  bool ensure_digit_gram() {
+    if (xg_valid_) return true;
+    if (xg_failed_ || !xsl_valid_ || !d_xsl || oz_kso() > 2 || !xsc_range_ok_) return false;
+    const int kso = oz_kso(), fpl = 4 * kso, np = fpl * (fpl + 1) / 2;
+    const uint64_t n_blocks = ldx / 16, n_chunks = (n_blocks + 3) / 4;
+    const uint64_t want = std::max<uint64_t>(1, (uint64_t)n_cu);
+    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(DG_MAX_CHUNKS, (n_chunks + want - 1) / want));
+    const int nwg = (int)std::max<uint64_t>(1, (n_chunks + per - 1) / per);
+    const size_t n_out = (size_t)OZ_SLICES * np * 256;
+    int* part = nullptr;
+    double* red = nullptr;
+    if (t_malloc((void**)&part, (size_t)nwg * n_out * sizeof(int)) != hipSuccess ||
+        t_malloc((void**)&red, n_out * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      if (part) (void)t_free(part);
+      xg_failed_ = true;  // the screen keeps its worst-case bound
+      return false;
+    }
+    if (kso == 2) k_digit_gram<2><<<nwg, 512, 0, stream>>>(d_xsl, n_blocks, per, part);
+    else k_digit_gram<1><<<nwg, 512, 0, stream>>>(d_xsl, n_blocks, per, part);
+    HIP_OK(hipGetLastError());
+    k_sum_islabs<<<(unsigned)((n_out + 255) / 256), 256, 0, stream>>>(part, nwg, n_out, red);
+    HIP_OK(hipGetLastError());
+    std::vector<double> g(n_out);
+    HIP_OK(hipMemcpyAsync(g.data(), red, n_out * sizeof(double), hipMemcpyDeviceToHost, stream));
+    sync();
+    HIP_OK(t_free(part));
+    HIP_OK(t_free(red));
+    ++n_digit_gram_;
+    // Gershgorin: λmax(D_b) ≤ max_f Σ_g |D_b[f][g]|. Tile pair (t1, t2), lane l, reg r holds
+    // D_b[fpl·i + t1][fpl·j + t2] with i = 4·(l >> 4) + r, j = l & 15 (and its mirror if t1 ≠ t2)
+    // Planes 0–3 (the pairs that dominate a D ≤ 2 or 3 screen's tail) also get Ostrowski's bound
+    // on the approximate eigenbasis V: λmax(D) ≤ λmax(VᵀDV)/σmin(V)², with λmax(VᵀDV) by
+    // Gershgorin (VᵀDV is nearly diagonal), σmin(V)² ≥ 1 − ‖VᵀV − I‖_F, and 1e-9·tr(D) for the
+    // rounding of VᵀDV (≤ n³·u·tr(D)); the smaller of the two bounds is kept.
+    const int nfp = fpl * 16;
+    std::vector<double> rs(nfp);
+    Mat dm(nfp, nfp);
+    for (int b = 0; b < OZ_SLICES; ++b) {
+      std::fill(rs.begin(), rs.end(), 0.0);
+      int p = 0;
+      for (int t1 = 0; t1 < fpl; ++t1)
+        for (int t2 = t1; t2 < fpl; ++t2, ++p)
+          for (int l = 0; l < 64; ++l)
+            for (int r = 0; r < 4; ++r) {
+              const double v = g[((size_t)(b * np + p) * 64 + l) * 4 + r];
+              const int i = 4 * (l >> 4) + r, j = l & 15;
+              rs[fpl * i + t1] += std::fabs(v);
+              if (t1 != t2) rs[fpl * j + t2] += std::fabs(v);
+              dm(fpl * i + t1, fpl * j + t2) = v;
+              dm(fpl * j + t2, fpl * i + t1) = v;
+            }
+      double mx = 0.0;
+      for (double v : rs) mx = std::max(mx, v);
+      xg_lam_[b] = mx * (1.0 + 1e-12);  // integer sums < 2^53: exact but for the last few adds
+      if (b > 3) continue;
+      std::vector<double> vals;
+      Mat v;
+      eigh(dm, &vals, &v);
+      Mat dv = matmul(dm, v), m(nfp, nfp), vtv(nfp, nfp);
+      for (int i = 0; i < nfp; ++i)
+        for (int j = 0; j < nfp; ++j) {
+          double s = 0.0, u = 0.0;
+          for (int k = 0; k < nfp; ++k) {
+            s += v(k, i) * dv(k, j);
+            u += v(k, i) * v(k, j);
+          }
+          m(i, j) = s;
+          vtv(i, j) = u - (i == j ? 1.0 : 0.0);
+        }
+      double eps = 0.0, tr = 0.0, gm = 0.0;
+      for (int i = 0; i < nfp; ++i) {
+        tr += dm(i, i);
+        double row = 0.0;
+        for (int j = 0; j < nfp; ++j) {
+          eps += vtv(i, j) * vtv(i, j);
+          row += std::fabs(m(i, j));
+        }
+        gm = std::max(gm, row);
+      }
+      eps = std::sqrt(eps) * (1.0 + 1e-6) + 1e-14;
+      if (eps < 0.5 && std::isfinite(gm)) {
+        const double ostrowski = (gm + 1e-9 * tr) / (1.0 - eps) * (1.0 + 1e-12);
+        xg_lam_[b] = std::min(xg_lam_[b], ostrowski);
+      }
+    }
+    xg_valid_ = true;
+    return true;
+  }
   // The digit G stage scales every y of a row by one power of two set by the image's LARGEST
   // sample exponent emax, so a typical sample keeps 2^(emax − e_typ) fewer bits of y (its X
   // digits carry their own 2^e_t; y's fixed point does not). Its G error grows by that factor
@@ -4031,7 +4134,8 @@ struct DeviceCtx : Evaluator {
     uint8_t* img = (uint8_t*)sc + WSC_BYTES;
     std::memset(img, 0, img_bytes);
     for (int i = 0; i < 256; ++i) sc[i] = 0x1p-12;
-    oz_split_rows(w, nc, nf, img, sc, ksw);  // host_linalg.cpp: rows split over the host threads
+    wsl_dn2_.assign(nc * OZ_SLICES, 0.0);
+    oz_split_rows(w, nc, nf, img, sc, ksw, wsl_dn2_.data());  // host_linalg.cpp: rows split over the host threads
     // fused_g8.inc: ysc_j = 2^(46 − F_j) with |y_jt| < 2^F_j for every sample:
     // |y_jt| ≤ Σ_k|W_jk|·max_k|X_kt| < 2^(ilogb(Σ|W_j|) + 1)·2^emax (Σ|W_j| taken 1e-12 high for its
     // own rounding; the digit forms of W and X and the fp64 combine stay within 2^-50 of it, and
@@ -4058,6 +4162,9 @@ struct DeviceCtx : Evaluator {
     HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + img_bytes, hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);  // the pinned images stay untouched until these copies are done
   }
+  // Σ_k w_a,ik² per row and digit level of the W in the image (upload_wsl) and of the paired
+  // screen's two W's (upload_wsl_pair): the screen's statistical bound
+  std::vector<double> wsl_dn2_, pair_dn2_[2];
   // two tries' W for the paired screen: w1 in row blocks 0 … NB − 1, w2 in NB … 2·NB − 1 (row
   // scales 0 … and 16·NB …), the layout k_screen_oz2<NB, ·, 2> reads
   void upload_wsl_pair(const double* w1, const double* w2, size_t nc, int nb) {
@@ -4069,8 +4176,10 @@ struct DeviceCtx : Evaluator {
     uint8_t* img = (uint8_t*)sc + WSC_BYTES;
     std::memset(img, 0, 2 * half);
     for (int i = 0; i < 512; ++i) sc[i] = 0x1p-12;
-    oz_split_rows(w1, nc, nf, img, sc, ksw);
-    oz_split_rows(w2, nc, nf, img + half, sc + 16 * nb, ksw);
+    pair_dn2_[0].assign(nc * OZ_SLICES, 0.0);
+    pair_dn2_[1].assign(nc * OZ_SLICES, 0.0);
+    oz_split_rows(w1, nc, nf, img, sc, ksw, pair_dn2_[0].data());
+    oz_split_rows(w2, nc, nf, img + half, sc + 16 * nb, ksw, pair_dn2_[1].data());
     wsl_nc_ = 0;  // the image no longer holds a single W
     HIP_OK(hipMemcpyAsync(d_wsc, sc, WSC_BYTES + 2 * half, hipMemcpyHostToDevice, stream));
     pin_release(pin_wsl_);
@@ -4163,10 +4272,16 @@ struct DeviceCtx : Evaluator {
   // Lipschitz in y (tanh: |ℓ′| = |tanh αy| ≤ 1; exp: |ℓ′| ≤ 1/√(αe)) each row's Σℓ
   // moves by at most Lip·2^(f_i−12)·B·Σ_t 2^e_t; 1e-10 of Σ_t|ℓ| covers the rounding
   // of both passes (their sums run in the same order). Ortho densities tanh / exp.
-  // diagonals the screen keeps: D ≤ 3 (10 digit products, 4 planes) by default; its bound is
-  // then ≈ 7× the D ≤ 4 screen's, which still decides every C3 rejection
-  // (PICARD_SCREEN_DMAX=4: 15 products, 5 planes)
-  int screen_dmax_ = std::getenv("PICARD_SCREEN_DMAX") && std::atoi(std::getenv("PICARD_SCREEN_DMAX")) == 4 ? 4 : 3;
+  // diagonals the first screen keeps: D ≤ 2 (6 digit products, 3 planes) by default, with the
+  // statistical tail bound (screen_rank_bound); a try it leaves undecided above the current loss
+  // goes to D ≤ 3 (10 products, 4 planes), then D ≤ 4 (15, 5) — eval_loss_screen_fine's levels.
+  // PICARD_SCREEN_DMAX=3 / 4 starts the chain there. A rank without the digit Grams (or the
+  // fp32 screen form) runs D ≤ 3 where D ≤ 2 is asked (same collectives; its bound is its own).
+  int screen_dmax_ = [] {
+    const char* e = std::getenv("PICARD_SCREEN_DMAX");
+    const int v = e ? std::atoi(e) : 2;
+    return v == 3 || v == 4 ? v : 2;
+  }();
   // fp32 ℓ in the tanh screen (loss_acc4_f32): hardware error constants, each at least the
   // exhaustive measurement of pc_device_check_fp32_transcendentals on MI355X (the -m gpu
   // test fails if a device exceeds them): v_exp_f32 relative on [−126, 0], absolute below;
@@ -4188,10 +4303,10 @@ struct DeviceCtx : Evaluator {
                         double* bound_out) override {
     return screen_at(screen_dmax_, w, nc, mu, d, ll_out, bound_out);
   }
-  // the finer screen: D ≤ 4 (only when the default is coarser)
-  bool eval_loss_screen_fine(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
+  // the finer screens: level 1, 2, … keep D ≤ screen_dmax_ + level, up to D ≤ 4
+  bool eval_loss_screen_fine(int level, const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
                              double* bound_out) override {
-    return screen_dmax_ < 4 && screen_at(4, w, nc, mu, d, ll_out, bound_out);
+    return level >= 1 && screen_dmax_ + level <= 4 && screen_at(screen_dmax_ + level, w, nc, mu, d, ll_out, bound_out);
   }
   // W row exponents (the kernels' f_i: 2^f_i > max_k |W_ik|; 0 for a zero row), and whether
   // the fp32 screen's scales 2^(f_i+e_t−20) all stay normal fp32 with room (see screen_at)
@@ -4209,8 +4324,19 @@ struct DeviceCtx : Evaluator {
       }
     }
   }
-  // this rank's part of the bound per row (screen_at's tail and fp32 terms)
-  void screen_rank_bound(int dmax, const std::vector<int>& fexp, size_t nc, pc_density d, bool f32l, double* bnd) const {
+  // This rank's part of the bound per row: the truncation tail and the fp32 terms. The exact
+  // stage's y differs from the screen's by Σ_{dmax < a+b ≤ 6} W_a,i·X_b,t (W_a,i = 2^(f_i−6−8a)·w_a,i,
+  // X_b,t = 2^(e_t−6−8b)·d_b,t: the digit levels), and ℓ is Lipschitz in y, so each row's Σℓ moves
+  // by at most Lip·Σ_(a,b) Σ_t |W_a,i·X_b,t|. Two rigorous bounds of that sum; the smaller is taken:
+  //  * worst case: every digit at its largest, 2^(f_i−12)·Σ_D 256^−D·max|P_D|·Σ_t 2^e_t;
+  //  * statistical (dn2 and the digit Grams present): Cauchy–Schwarz over t with the weights
+  //    2^e_t, Σ_t 2^e_t·|w_a,i·d_b,t| ≤ √(Σ_t 4^e_t)·√(w_a,i·D_b·w_a,iᵀ) ≤ √(S4·λ_b·‖w_a,i‖²)
+  //    (D_b the exact digit Gram, λ_b ≥ its largest eigenvalue) — ≈ 30× smaller on the bench
+  //    mixtures, which lets a D ≤ 2 screen decide what the worst case needed D ≤ 3 for.
+  // f32l: the fp32 combine's absolute term (fl(R23), D ≥ 3 only: |P_2| < 2^24 is exact in fp32)
+  // and the fp32 ℓ terms per 4-sample block.
+  void screen_rank_bound(int dmax, const std::vector<int>& fexp, const double* dn2, size_t nc, pc_density d,
+                         bool f32l, double* bnd) const {
     auto pm = [](int dd) {  // Σ_{a+b=dd} |d_a|max·|d_b|max per feature
       double v = 0.0;
       for (int a = 0; a < OZ_SLICES; ++a) {
@@ -4219,13 +4345,25 @@ struct DeviceCtx : Evaluator {
       }
       return v;
     };
-    double bsum = 0.0;
+    double bsum = 0.0, bf32 = 0.0;
     for (int dd = dmax + 1; dd <= OZ_SLICES - 1; ++dd) bsum += std::ldexp(pm(dd), -8 * dd);  // exact stage: D ≤ 6
-    if (f32l) bsum += std::ldexp(256.0 * pm(2) + pm(3) + pm(4) / 256.0, -46) * (1.0 + 1e-6);
+    if (f32l && dmax >= 3) bf32 = std::ldexp(256.0 * pm(2) + pm(3) + pm(4) / 256.0, -46) * (1.0 + 1e-6);
     const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
-    const double tail = (double)nf * bsum * xsc_sum_ * lip;
+    const double worst = (double)nf * bsum * xsc_sum_ * lip, f32abs = (double)nf * bf32 * xsc_sum_ * lip;
+    const bool stat = dn2 != nullptr && xg_valid_;
     for (size_t i = 0; i < nc; ++i) {
-      bnd[i] = std::ldexp(tail, fexp[i] - 12) * (1.0 + 1e-12);
+      double tail = worst;
+      if (stat) {
+        double st = 0.0;
+        for (int a = 0; a < OZ_SLICES; ++a)
+          for (int b = 0; b < OZ_SLICES; ++b) {
+            const int dd = a + b;
+            if (dd > dmax && dd <= OZ_SLICES - 1)
+              st += std::ldexp(std::sqrt(dn2[i * OZ_SLICES + a] * xg_lam_[b] * xsc_s4_), -8 * dd);
+          }
+        tail = std::min(tail, st * lip * (1.0 + 1e-9));  // (1e-9: the rounding of these few ops)
+      }
+      bnd[i] = std::ldexp(tail + f32abs, fexp[i] - 12) * (1.0 + 1e-12);
       if (f32l) bnd[i] += (double)(ldx / 4) * screen_f32_block_bound(d.alpha);
     }
   }
@@ -4243,7 +4381,7 @@ struct DeviceCtx : Evaluator {
   // kernel arithmetic per W, the same bound terms.
   bool eval_loss_screen2(const double* w1, const double* w2, size_t nc, const double* mu, pc_density d, double* ll1,
                          double* bnd1, double* ll2, double* bnd2) override {
-    if (!screen_pairs_ || screen_dmax_ != 3 || !screen_nows_ || !screen_v2_ || !screen_f32_) return false;
+    if (!screen_pairs_ || screen_dmax_ > 3 || !screen_nows_ || !screen_v2_ || !screen_f32_) return false;
     if (y_stage_ != 0 || !oz_any(nc) || !(d.alpha > 0.0) || d.kind != DENS_TANH) return false;
     std::vector<int> f1, f2;
     bool w_ok = true;
@@ -4267,17 +4405,21 @@ struct DeviceCtx : Evaluator {
               xsc_emax_ <= PAIR_EMAX;
     if (coll_) ok = agree_once(screen_pair_agreed_, ok, "the paired line-search screen");
     if (!ok) return false;
+    // D ≤ 2 where this rank has the digit Grams (else D ≤ 3: the same collectives)
+    const int dmax = screen_dmax_ == 2 && ensure_digit_gram() ? 2 : 3;
     upload_wsl_pair(w1, w2, nc, nb);
     d_wsl_ready_ = false;  // the image holds two W's: no completion may reuse it
     kept_nc_pending = nc;
     HIP_OK(hipEventRecord(ev[0], stream));
     double* direct = direct_acquire(6 * nc);
     if (direct) st_rows = direct;
-    const bool launched = nb4 ? launch_screen_oz2<4>(d.alpha, st_rows, 2) : launch_screen_oz2<8>(d.alpha, st_rows, 2);
+    const bool launched =
+        nb4 ? launch_screen_oz2<4>(d.alpha, st_rows, 2, dmax) : launch_screen_oz2<8>(d.alpha, st_rows, 2, dmax);
     if (!launched) throw computation_error("paired screen: launch geometry out of range after the agreement");
     double* bnd = direct ? direct : (double*)pin_acquire(pin_in_, 6 * nc * sizeof(double));
-    screen_rank_bound(3, f1, nc, d, true, bnd + 2 * nc);
-    screen_rank_bound(3, f2, nc, d, true, bnd + 5 * nc);
+    screen_rank_bound(dmax, f1, pair_dn2_[0].data(), nc, d, true, bnd + 2 * nc);
+    screen_rank_bound(dmax, f2, pair_dn2_[1].data(), nc, d, true, bnd + 5 * nc);
+    n_screen_products += 2 * (uint64_t)((dmax + 1) * (dmax + 2) / 2);
     std::vector<double> tmp(6 * nc);
     const double* staged = direct;
     if (direct) {
@@ -4344,33 +4486,17 @@ struct DeviceCtx : Evaluator {
     bool f32l = d.kind == DENS_TANH && screen_f32_ && xsc_range_ok_;
     for (size_t i = 0; f32l && i < nc; ++i)
       if (!zero_row[i] && (fexp[i] - 20 + xsc_emin_ < -100 || fexp[i] - 20 + xsc_emax_ > 99)) f32l = false;
+    // D ≤ 2 only with this rank's digit Grams (its worst-case tail is ≈ 190× D ≤ 3's)
+    if (dmax == 2 && !ensure_digit_gram()) dmax = 3;
     HIP_OK(hipEventRecord(ev[0], stream));
     direct = direct_acquire(3 * nc);  // (after the image checks: no early return holds the slot)
     if (direct) st_rows = direct;
-    if (nb4) screen_launch<4>(d, dmax, f32l, st_rows);
-    else screen_launch<8>(d, dmax, f32l, st_rows);
-    // B = Σ_{D > DMAX} 256^−D · max|P_D| / nf
-    auto pm = [](int dd) {  // Σ_{a+b=dd} |d_a|max·|d_b|max per feature
-      double v = 0.0;
-      for (int a = 0; a < OZ_SLICES; ++a) {
-        const int b = dd - a;
-        if (b >= 0 && b < OZ_SLICES) v += (a == 0 ? 65.0 : 128.0) * (b == 0 ? 65.0 : 128.0);
-      }
-      return v;
-    };
-    double bsum = 0.0;
-    for (int dd = dmax + 1; dd <= OZ_SLICES - 1; ++dd) bsum += std::ldexp(pm(dd), -8 * dd);  // exact stage: D ≤ 6
-    // fp32 combine (oz_combine_screen_f32): the absolute part 2^-38·(|R23| + |P_4|/256)·2^(f_i+e_t−20)
-    if (f32l) bsum += std::ldexp(256.0 * pm(2) + pm(3) + pm(4) / 256.0, -46) * (1.0 + 1e-6);
-    const double lip = d.kind == DENS_TANH ? 1.0 : 1.0 / std::sqrt(d.alpha * std::exp(1.0));
-    const double tail = (double)nf * bsum * xsc_sum_ * lip;
+    dmax = nb4 ? screen_launch<4>(d, dmax, f32l, st_rows) : screen_launch<8>(d, dmax, f32l, st_rows);
+    n_screen_products += (uint64_t)((dmax + 1) * (dmax + 2) / 2);
     // this rank's bound: summed over ranks with the statistics (its own row of the all-reduce)
+    // (fp32 ℓ: 4 lane-blocks of 4 samples per 16-sample block of each row, padding included)
     double* bnd = direct ? direct + 2 * nc : (double*)pin_acquire(pin_in_, nc * sizeof(double));  // H2D by DMA
-    for (size_t i = 0; i < nc; ++i) {
-      bnd[i] = std::ldexp(tail, fexp[i] - 12) * (1.0 + 1e-12);
-      // fp32 ℓ: 4 lane-blocks of 4 samples per 16-sample block of this row (padding included)
-      if (f32l) bnd[i] += (double)(ldx / 4) * screen_f32_block_bound(d.alpha);
-    }
+    screen_rank_bound(dmax, fexp, wsl_dn2_.size() == nc * OZ_SLICES ? wsl_dn2_.data() : nullptr, nc, d, f32l, bnd);
     std::vector<double> tmp(3 * nc);
     const double* staged = direct;
     if (direct) {
@@ -4425,10 +4551,10 @@ struct DeviceCtx : Evaluator {
   bool screen_v2_ = !(std::getenv("PICARD_SCREEN_V2") && std::atoi(std::getenv("PICARD_SCREEN_V2")) == 0);
   bool screen32_ = std::getenv("PICARD_SCREEN32") && std::atoi(std::getenv("PICARD_SCREEN32")) == 1;
   template <int NB>
-  bool launch_screen_oz2(double alpha, double* st_rows, int nw = 1) {
+  bool launch_screen_oz2(double alpha, double* st_rows, int nw = 1, int dmax = 3) {
     constexpr int NCP = 16 * NB;
     // k_screen_oz32 (PICARD_SCREEN32=1): one try at NB = 8, two blocks per step, one workgroup per CU
-    const bool f32form = screen32_ && NB == 8 && nw == 1;
+    const bool f32form = screen32_ && NB == 8 && nw == 1 && dmax == 3;
     const int U = f32form ? 2 : screen2_blocks_per_step(NB);
     const uint64_t n_blocks = (n_local_ + 15) / 16;
     const uint64_t want =
@@ -4450,6 +4576,7 @@ struct DeviceCtx : Evaluator {
     a.bpw = (uint32_t)bpw; a.n_blocks = (uint32_t)n_blocks; a.nwg = nwg; a.partials = part;
     a.nw = nw;
     a.form32 = f32form;
+    a.dmax = dmax;
     HIP_OK(hipEventRecord(ev[1], stream));
     HIP_OK(screen2_launch(NB, a, stream));
     HIP_OK(hipEventRecord(ev[2], stream));
@@ -4464,9 +4591,17 @@ struct DeviceCtx : Evaluator {
     ++n_screen_passes_;
     return true;
   }
+  // returns the diagonals the launched screen keeps (D ≤ 2 is k_screen_oz2's only: elsewhere 3)
   template <int NB>
-  void screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
-    if (f32l && dmax == 3 && screen_nows_ && screen_v2_ && launch_screen_oz2<NB>(d.alpha, st_rows)) return;
+  int screen_launch(pc_density d, int dmax, bool f32l, double* st_rows) {
+    if (f32l && dmax <= 3 && screen_nows_ && screen_v2_ && launch_screen_oz2<NB>(d.alpha, st_rows, 1, dmax))
+      return dmax;
+    if (dmax < 3) dmax = 3;
+    screen_launch_other<NB>(d, dmax, f32l, st_rows);
+    return dmax;
+  }
+  template <int NB>
+  void screen_launch_other(pc_density d, int dmax, bool f32l, double* st_rows) {
     if (f32l && dmax == 3 && screen_nows_) launch_screen_oz<3, NB>(d.alpha, st_rows);
     else if (f32l && dmax == 3) launch_loss_oz<DENS_TANH, false, 3, true, NB>(d.alpha, false, st_rows);
     else if (f32l) launch_loss_oz<DENS_TANH, false, 4, true, NB>(d.alpha, false, st_rows);
@@ -4563,6 +4698,7 @@ struct DeviceCtx : Evaluator {
     if (kind == 4) { sum_screen_ms += a; ++n_screen; ++n_screen_tries; }
   }
   uint64_t n_screen_tries = 0;  // tries the screen passes covered (a paired pass: 2)
+  uint64_t n_screen_products = 0;  // Σ over those tries of the digit products each kept ((D+1)(D+2)/2)
   double sum_split_ms = 0;
   uint64_t n_split = 0;
 
@@ -5164,13 +5300,22 @@ void device_ctx_set_y_stage(Evaluator* e, int mode) {
   d->y_stage_ = mode;
 }
 uint64_t device_ctx_int8_passes(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_int8_passes_; }
+// the screen's statistical-bound inputs (tests): false without an int8 digit image
+bool device_ctx_screen_digit_gram(Evaluator* e, double* lam, double* s4) {
+  DeviceCtx* c = static_cast<DeviceCtx*>(e);
+  if (!c->ensure_xsl() || !c->ensure_digit_gram()) return false;
+  for (int b = 0; b < OZ_SLICES; ++b) lam[b] = c->xg_lam_[b];
+  *s4 = c->xsc_s4_;
+  return true;
+}
 void device_ctx_screen_stats(Evaluator* e, double* ms, uint64_t* n, int reset) {
   auto* d = static_cast<DeviceCtx*>(e);
   *ms = d->sum_screen_ms;
   *n = d->n_screen;
-  if (reset) { d->sum_screen_ms = 0; d->n_screen = 0; d->n_screen_tries = 0; }
+  if (reset) { d->sum_screen_ms = 0; d->n_screen = 0; d->n_screen_tries = 0; d->n_screen_products = 0; }
 }
 uint64_t device_ctx_screen_tries(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_screen_tries; }
+uint64_t device_ctx_screen_products(const Evaluator* e) { return static_cast<const DeviceCtx*>(e)->n_screen_products; }
 void device_check_f32_transc(int device, double* out4) {
   HIP_OK(hipSetDevice(device));
   const int nblk = 2048;

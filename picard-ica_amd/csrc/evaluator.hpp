@@ -115,11 +115,12 @@ class Evaluator {
     (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
     return false;
   }
-  // The same on a finer (slower, tighter) approximation, for tries the default screen left
-  // undecided although its estimate lies above the current loss. false = none.
-  virtual bool eval_loss_screen_fine(const double* w, size_t nc, const double* mu, pc_density d, double* ll_out,
-                                     double* bound_out) {
-    (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
+  // The same on finer (slower, tighter) approximations, level 1, 2, … in turn, for tries the
+  // screens so far left undecided although their estimate lies above the current loss.
+  // false = no such level. Rank-independent availability (the levels issue collectives).
+  virtual bool eval_loss_screen_fine(int level, const double* w, size_t nc, const double* mu, pc_density d,
+                                     double* ll_out, double* bound_out) {
+    (void)level; (void)w; (void)nc; (void)mu; (void)d; (void)ll_out; (void)bound_out;
     return false;
   }
   // Two tries' screens in one pass (w1, w2: the same shape): each try's [Σℓ, bound] exactly as

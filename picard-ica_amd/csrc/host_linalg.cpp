@@ -615,7 +615,9 @@ bool invert_matrix(const Mat& m, Mat* out) {
 // of 64·w·2^-f_i by a shifter rint (exact for |v| < 2^51), ±128/±129 folded into the digit
 // above; img[wave][digit][kstep][lane][16 B] as the i8 MFMA B operand. A NaN / ±inf weight
 // makes the row's scale NaN (zero digits), as the fp64 stage would give NaN.
-void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc, int ksw) {
+// dn2 (optional, [nc][7]): Σ_k w_a,ik² per row and digit level a (exact integers), for the
+// line-search screen's statistical bound (DeviceCtx::screen_rank_bound).
+void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc, int ksw, double* dn2) {
   constexpr double SH = 0x1.8p52;
   constexpr int OZ_SLICES = 7;
   // rows are independent (each writes its own digit bytes and scale): split over the threads
@@ -629,6 +631,8 @@ void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* 
       bad |= !std::isfinite(w[i * nf + k]);
       mx = f > mx ? f : mx;  // = fmax (NaN rows are flagged by bad), without a libm call
     }
+    if (dn2)
+      for (int a = 0; a < OZ_SLICES; ++a) dn2[i * OZ_SLICES + a] = 0.0;
     if (bad) {
       sc[i] = std::nan("");
       continue;  // zero digits
@@ -654,6 +658,8 @@ void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* 
       const size_t s = k >> 6, lane = n + 16 * ((k >> 4) & 3), j = k & 15;
       for (int a = 0; a < OZ_SLICES; ++a)
         img[(((wave * OZ_SLICES + a) * ksw + s) * 64 + lane) * 16 + j] = (uint8_t)(int8_t)dg[a];
+      if (dn2)
+        for (int a = 0; a < OZ_SLICES; ++a) dn2[i * OZ_SLICES + a] += (double)(dg[a] * dg[a]);
     }
   }
 }

@@ -34,7 +34,7 @@ Mat scale(const Mat& a, double s);
 double max_abs(const Mat& a);
 // int8 digit image of W rows for the device Y stage (host_linalg.cpp)
 // image [row block][digit][k-step < ksw][lane][16 B] (ksw = 2 for nf ≤ 128, 4 for nf ≤ 256)
-void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc, int ksw);
+void oz_split_rows(const double* w, size_t nc, size_t nf, uint8_t* img, double* sc, int ksw, double* dn2 = nullptr);
 double dot_sum(const Mat& a, const Mat& b);       // Σ a∘b
 
 // Symmetric eigendecomposition (cyclic Jacobi). Eigenvalues ascending (as

@@ -938,11 +938,11 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           std::fprintf(stderr, "[picard-screen] try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s%s\n", k + 1, alpha,
                        lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact", via);
         // undecided, but the estimate lies above the current loss (a likely rejection): the
-        // finer screen first, when the evaluator has one, before the full pass. Its inputs
-        // are the reduced statistics, so every rank takes the same branch.
-        const double tf = now_ms();
-        if (!rejected && lo + eb > current_loss_ &&
-            ev_->eval_loss_screen_fine(wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) {
+        // finer screens in turn, while the evaluator has them, before the full pass. Their
+        // inputs are the reduced statistics, so every rank takes the same branch.
+        for (int level = 1; !rejected && lo + eb > current_loss_; ++level) {
+          const double tf = now_ms();
+          if (!ev_->eval_loss_screen_fine(level, wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) break;
           eval_ms_ += now_ms() - tf;  // device time (host_ms counted it before round 5)
           ++screen_passes_;
           lo = 0.0;
@@ -953,8 +953,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
           }
           rejected = !(lo < current_loss_);
           if (trace_)
-            std::fprintf(stderr, "[picard-screen] fine try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", k + 1,
-                         alpha, lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact");
+            std::fprintf(stderr, "[picard-screen] fine%d try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", level,
+                         k + 1, alpha, lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb,
+                         rejected ? "reject" : "exact");
         }
       }
       if (rejected) {

@@ -1,5 +1,5 @@
 // The orthogonal line-search screen, second form (k_screen_oz2): the same bound as
-// k_screen_oz (ozaki.inc) — diagonals D ≤ 3 of the exact int8 digit stage, the fp32 combine
+// k_screen_oz (ozaki.inc) — diagonals D ≤ 3 (or D ≤ 2, DeviceCtx::screen_at) of the exact int8 digit stage, the fp32 combine
 // and fp32 ℓ with the error terms DeviceCtx::screen_at adds — on a schedule built from the
 // issue costs measured on MI355X (tools/microbench/fill_coexec.hip, profiles/r04_a):
 //
@@ -54,12 +54,19 @@ __device__ __forceinline__ v4i mfma_i8(v4i a, v4i b, v4i c) {
 // as loss_acc4_f32y, negated), then Σ|u| in fp32 ((|u0| + |u1|) + (|u2| + |u3|)) into l and
 // log2 Π (1 + 2^−z)/2 into g — every rounding of loss_acc4_f32y's per-element arithmetic, on
 // values scaled by exact powers of two.
+template <int DM>
 __device__ __forceinline__ void row_terms(const v4i (&acc)[4], const f4v& sf, float cz, double& l, double& g) {
+  static_assert(DM == 2 || DM == 3, "screen diagonals");
   float u[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int q01 = acc[0][r] * 256 + acc[1][r], r23 = acc[2][r] * 256 + acc[3][r];
-    u[r] = __builtin_fmaf((float)r23, 0x1p-16f, (float)q01) * sf[r];
+    const int q01 = acc[0][r] * 256 + acc[1][r];
+    if constexpr (DM == 3) {
+      const int r23 = acc[2][r] * 256 + acc[3][r];
+      u[r] = __builtin_fmaf((float)r23, 0x1p-16f, (float)q01) * sf[r];
+    } else {  // |P_2| < 2^24: exact in fp32, so the fma is the only rounding after fl(Q01)
+      u[r] = __builtin_fmaf((float)acc[2][r], 0x1p-8f, (float)q01) * sf[r];
+    }
   }
   float f[4];
 #pragma unroll
@@ -69,15 +76,16 @@ __device__ __forceinline__ void row_terms(const v4i (&acc)[4], const f4v& sf, fl
   g += (double)__builtin_amdgcn_logf((f[0] * f[1]) * (f[2] * f[3]));
 }
 
-template <int NB>
+template <int NB, int DM = 3>
 struct S2 {
   static constexpr int KSO = NB == 8 ? 2 : 1;          // k-steps of 64 features
   static constexpr int U = 8 / NB;                     // 16-sample blocks per step
   static constexpr int NCP = 16 * NB;                  // rows of the partials
   static constexpr int TILE = SLICES * KSO * 1024;     // bytes of one block's digit image
-  static constexpr int PL = 4;                         // digit planes the screen reads (D ≤ 3)
+  static constexpr int PL = DM + 1;                    // digit planes the screen reads (D ≤ DM)
   static constexpr int SLOT = PL * KSO * 1024;         // LDS bytes of one block's planes
-  static constexpr int PIECES = PL * KSO;              // 1-KiB pieces per block (U·PIECES = 8)
+  static constexpr int PIECES = PL * KSO;              // 1-KiB pieces per block (U·PIECES ≤ 8)
+  static constexpr int NPROD = (DM + 1) * (DM + 2) / 2;  // digit products per k-step (a + b ≤ DM)
   static constexpr int NBUF = 3, SCB = 256;
   template <int NW>
   static constexpr int lds() { return NBUF * U * SLOT + NBUF * SCB + NW * U * NCP * 2 * 8; }
@@ -89,14 +97,14 @@ struct S2 {
 // arithmetic and order of NW = 1 (so each W's sums are bit-identical to its own screen), partials
 // [nwg][NW][2·NCP]. Half the HBM bytes per try: the screen's clock is held down by the memory
 // side's power (profiles/r04_e/screen_clock.txt), and two tries per pass relieve it.
-template <int NB, int FILL, int NW>
+template <int NB, int FILL, int NW, int DM>
 __global__ void __launch_bounds__(512, NW == 1 ? 2 : 1)
 k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, const uint8_t* __restrict__ wsl_g,
              const double* __restrict__ wsc, float c32, int e0, double ln2_alpha, uint32_t bpw, uint32_t n_blocks,
              double* __restrict__ partials) {
-  using S = S2<NB>;
-  constexpr int KSO = S::KSO, U = S::U, NCP = S::NCP, TILE = S::TILE, SLOT = S::SLOT, NBUF = S::NBUF;
-  static_assert(U * S::PIECES == 8, "one piece per wave and step");
+  using S = S2<NB, DM>;
+  constexpr int KSO = S::KSO, U = S::U, NCP = S::NCP, TILE = S::TILE, SLOT = S::SLOT, NBUF = S::NBUF, PL = S::PL;
+  static_assert(U * S::PIECES <= 8, "at most one piece per wave and step");
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lr = lane & 15, lk = lane >> 4;
@@ -116,15 +124,18 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
       uniform_ptr(xsl + (size_t)b_begin * TILE), 0, __builtin_amdgcn_readfirstlane((int)(nb * TILE)), RSRC_DW3);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(xsf + (size_t)b_begin * 16), 0, __builtin_amdgcn_readfirstlane((int)(nb * 64)), RSRC_DW3);
-  // this wave's piece of every step: block bp of the step, piece q (planes 0–3 are the first
-  // PL·KSO KiB of a block image); wave 7 also moves the step's U·16 scales (lanes repeat)
-  const int bp = wv / S::PIECES, q = wv % S::PIECES;
+  // this wave's piece of every step: block bp of the step, piece q (planes 0 … DM are the first
+  // PL·KSO KiB of a block image; D ≤ 2: waves 6, 7 stage no piece); wave 7 also moves the
+  // step's U·16 scales (lanes repeat)
+  const bool piece_wave = wv < U * S::PIECES;
+  const int bp = piece_wave ? wv / S::PIECES : 0, q = piece_wave ? wv % S::PIECES : 0;
   const uint32_t voff_x = (uint32_t)(bp * TILE + q * 1024 + lane * 16);
   const uint32_t voff_s = (uint32_t)((lane & (16 * U - 1)) * 4);
   const bool scale_wave = wv == 7;
   auto stage = [&](uint32_t step, int buf) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bp) * SLOT + q * 1024), 16,
-                                             (int)(voff_x + step * (uint32_t)(U * TILE)), 0, 0, 0);
+    if (piece_wave)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_vptr2)(tiles + (buf * U + bp) * SLOT + q * 1024), 16,
+                                               (int)(voff_x + step * (uint32_t)(U * TILE)), 0, 0, 0);
     if (scale_wave)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr2)(scl + buf * S::SCB), 4,
                                                (int)(voff_s + step * (uint32_t)(U * 64)), 0, 0, 0);
@@ -133,9 +144,12 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   // step after may still fly: counted vmcnt), then every wave meets
   // (lgkmcnt(0): this step's scale read has returned before the next step's DMA may overwrite
   // its buffer)
+  // (loads this wave issues per step: its piece and / or the scales)
+  const int per_step = (piece_wave ? 1 : 0) + (scale_wave ? 1 : 0);
   auto step_barrier = [&]() {
-    if (scale_wave) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+    if (per_step == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    else if (per_step == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
   v4i wsl[NW][4][KSO];
@@ -145,7 +159,7 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   for (int w = 0; w < NW; ++w) {
     const int rb = yi + NB * w;  // this try's row block in the W image
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a <= DM; ++a)
 #pragma unroll
       for (int s = 0; s < KSO; ++s)
         wsl[w][a][s] = *(const v4i*)(wsl_g + (size_t)(((rb * SLICES + a) * 2 + s) * 64 + lane) * 16);
@@ -164,8 +178,9 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   sf[1] = f4v{0.f, 0.f, 0.f, 0.f};
   stage(0, 0);
   stage(1, 1);
-  if (scale_wave) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  if (per_step == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (per_step == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   // step k: stage k + 2; the MFMAs of step k with the row terms of step k − 1 between them
   auto body = [&](uint32_t k, int buf, auto cur_c) {
@@ -176,14 +191,14 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
 #pragma unroll
     for (int s = 0; s < KSO; ++s) xa[0][s] = *(const v4i*)(tile + s * 1024);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      if (b < 3)
+    for (int b = 0; b < PL; ++b) {
+      if (b < PL - 1)
 #pragma unroll
         for (int s = 0; s < KSO; ++s) xa[(b + 1) & 1][s] = *(const v4i*)(tile + ((b + 1) * KSO + s) * 1024);
 #pragma unroll
       for (int s = 0; s < KSO; ++s)
 #pragma unroll
-        for (int a = 0; a <= 3 - b; ++a)
+        for (int a = 0; a <= DM - b; ++a)
 #pragma unroll
           for (int w = 0; w < NW; ++w) {
             const int d = a + b;
@@ -192,12 +207,12 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
           }
     }
 #pragma unroll
-    for (int w = 0; w < NW; ++w) row_terms(acc[prv][w], sf[prv], cz[w], l[w], g[w]);
+    for (int w = 0; w < NW; ++w) row_terms<DM>(acc[prv][w], sf[prv], cz[w], l[w], g[w]);
     sf[cur] = *(const f4v*)(scl + buf * S::SCB + h * 64 + lk * 16);
-    // one MFMA, then FILL vector instructions, over the 10·KSO·NW MFMAs of the step
+    // one MFMA, then FILL vector instructions, over the NPROD·KSO·NW MFMAs of the step
     if constexpr (FILL > 0) {
 #pragma unroll
-      for (int i = 0; i < 10 * KSO * NW; ++i) {
+      for (int i = 0; i < S::NPROD * KSO * NW; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, FILL, 0);
       }
@@ -219,10 +234,10 @@ k_screen_oz2(const uint8_t* __restrict__ xsl, const float* __restrict__ xsf, con
   if (k < nsteps) {
     body(k, buf, std::integral_constant<int, 0>{});
 #pragma unroll
-    for (int w = 0; w < NW; ++w) row_terms(acc[0][w], sf[0], cz[w], l[w], g[w]);
+    for (int w = 0; w < NW; ++w) row_terms<DM>(acc[0][w], sf[0], cz[w], l[w], g[w]);
   } else {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) row_terms(acc[1][w], sf[1], cz[w], l[w], g[w]);
+    for (int w = 0; w < NW; ++w) row_terms<DM>(acc[1][w], sf[1], cz[w], l[w], g[w]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero pieces past the end: drained
 #pragma unroll
@@ -434,18 +449,18 @@ __global__ void __launch_bounds__(256) k_build_xsf(const double* __restrict__ xs
   }
 }
 
-template <int NB, int FILL, int NW>
+template <int NB, int FILL, int NW, int DM>
 hipError_t launch_fill(const Screen2Args& a, hipStream_t stream) {
-  using S = S2<NB>;
+  using S = S2<NB, DM>;
   constexpr int LDS = S::template lds<NW>();
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB, FILL, NW>,
+    const hipError_t e = hipFuncSetAttribute((const void*)k_screen_oz2<NB, FILL, NW, DM>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  k_screen_oz2<NB, FILL, NW><<<a.nwg, 512, LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
+  k_screen_oz2<NB, FILL, NW, DM><<<a.nwg, 512, LDS, stream>>>(a.xsl, a.xsf, a.wsl, a.wsc, a.c32, a.e0, a.ln2_alpha,
                                                            a.bpw, a.n_blocks, a.partials);
   return hipGetLastError();
 }
@@ -459,19 +474,25 @@ int fill_knob() {
   }();
   return v;
 }
+template <int NB, int NW, int DM>
+hipError_t launch_dm(const Screen2Args& a, hipStream_t stream) {
+  switch (fill_knob()) {
+    case 0: return launch_fill<NB, 0, NW, DM>(a, stream);
+    case 2: return launch_fill<NB, 2, NW, DM>(a, stream);
+    default: return launch_fill<NB, 1, NW, DM>(a, stream);
+  }
+}
 template <int NB, int NW>
 hipError_t launch(const Screen2Args& a, hipStream_t stream) {
-  switch (fill_knob()) {
-    case 0: return launch_fill<NB, 0, NW>(a, stream);
-    case 2: return launch_fill<NB, 2, NW>(a, stream);
-    default: return launch_fill<NB, 1, NW>(a, stream);
-  }
+  if (a.dmax == 2) return launch_dm<NB, NW, 2>(a, stream);
+  if (a.dmax == 3) return launch_dm<NB, NW, 3>(a, stream);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
 
 int screen2_blocks_per_step(int nb) { return 8 / nb; }
-uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }
+uint64_t screen2_tile_bytes(int nb) { return nb == 8 ? S2<8>::TILE : S2<4>::TILE; }  // (all planes: DM-free)
 
 template <int FILL>
 hipError_t screen32_launch_fill(const Screen2Args& a, hipStream_t stream) {
@@ -501,7 +522,7 @@ hipError_t screen32_launch(const Screen2Args& a, hipStream_t stream) {
 }
 
 hipError_t screen2_launch(int nb, const Screen2Args& a, hipStream_t stream) {
-  if (a.form32) return nb == 8 && a.nw == 1 ? screen32_launch(a, stream) : hipErrorInvalidValue;
+  if (a.form32) return nb == 8 && a.nw == 1 && a.dmax == 3 ? screen32_launch(a, stream) : hipErrorInvalidValue;
   if (a.nw == 2) return nb == 8 ? launch<8, 2>(a, stream) : launch<4, 2>(a, stream);
   return nb == 8 ? launch<8, 1>(a, stream) : launch<4, 1>(a, stream);
 }

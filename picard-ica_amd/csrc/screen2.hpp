@@ -23,6 +23,7 @@ struct Screen2Args {
   double* partials;    // [nwg][nw][2·16·NB]: [Σℓ raw | Σ|ỹ|] per row
   int nw = 1;          // tries per pass: 2 = the second W in row blocks NB … 2·NB − 1 of the W image
   bool form32 = false; // k_screen_oz32 (NB = 8, nw = 1): 32x32x32 MFMAs, 2 blocks per step, 1 WG per CU
+  int dmax = 3;        // diagonals a + b ≤ dmax of the digit products (2: 6 products on planes 0–2; 3: 10 on 0–3)
 };
 
 int screen2_blocks_per_step(int nb);   // 16-sample blocks per loop step (NB = 8: 1, NB = 4: 2)

@@ -96,5 +96,5 @@ def test_error_names(pa):
     assert [pa.lib.pc_error_name(i).decode() for i in range(7)] == [
         "Ok", "InvalidDimensions", "SingularMatrix", "ComputationError", "InvalidConfig", "NotConverged",
         "Unsupported"]
-    assert pa.lib.pc_abi_version() == 7
+    assert pa.lib.pc_abi_version() == 8
     assert issubclass(pa.Unsupported, pa.ComputationError) and pa.Unsupported.code == 6

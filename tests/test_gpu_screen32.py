@@ -66,11 +66,12 @@ def test_f32_screen_bound_covers_exact(pa, n, alpha, dmax, monkeypatch):
 
 
 @pytest.mark.parametrize("tiny", [1e-35, 1e-25])
-def test_f32_screen_scale_range(pa, tiny):
+def test_f32_screen_scale_range(pa, tiny, monkeypatch):
     """The fp32 screen forms |ỹ| = |Y'|·2^(f_i+e_t−20) in fp32, which needs every scale in the
     normal fp32 range (DeviceCtx::screen_at checks the digit image's exponent range): a sample
     of size 1e-35 takes the rank to the fp64-ℓ screen, one of 1e-25 keeps the fp32 screen; the
     bound covers the exact pass either way."""
+    monkeypatch.setenv("PICARD_SCREEN_DMAX", "3")  # the D ≤ 3 bound's tightness is asserted
     rng = np.random.default_rng(5)
     n = 96
     x = _laplace_mix(rng, n, 20011)

@@ -24,6 +24,7 @@ def _mix(rng, n, t):
 @pytest.mark.parametrize("alpha", [1.0, 0.5])
 @pytest.mark.parametrize("t", [30011, 4099])
 def test_screen32_bound_covers_exact(pa, n, alpha, t, monkeypatch):
+    monkeypatch.setenv("PICARD_SCREEN_DMAX", "3")  # the 32x32x32 form is a D ≤ 3 screen
     rng = np.random.default_rng(n + t)
     x = _mix(rng, n, t)
     x[:, 7] *= 1e3  # one loud sample
@@ -54,6 +55,7 @@ def test_screen32_bound_covers_exact(pa, n, alpha, t, monkeypatch):
 def test_screen32_fit_bit_identical(pa, seed, monkeypatch):
     """Picard-O at N = 96 on the int8 stage: the fit screened on k_screen_oz32 takes the same
     decisions as the exact mode (every try evaluated in full)."""
+    monkeypatch.setenv("PICARD_SCREEN_DMAX", "3")
     rng = np.random.default_rng(seed)
     x = _mix(rng, 96, 40011)
     cfg = dict(max_iter=60, random_state=seed)
