@@ -646,6 +646,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
   // a paired screen's second try (Evaluator::eval_loss_screen2): its rows, for try pair_k
   std::vector<double> pair_ll, pair_bnd;
   size_t pair_k = tries;
+  // the previous screened try of this search: its margin (estimate − current loss) and the
+  // bound of its first-level screen (schedule only, below)
+  double prev_margin = -1.0, prev_eb0 = 0.0;
   for (size_t k = 0; k < tries; ++k) {
     Mat transform;
     if (ortho) {
@@ -892,7 +895,23 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       const double* mu = has_mu_ ? mu_.data() : nullptr;
       bool got = false;
       const char* via = "";
-      if (pair_k == k) {  // screened with the previous try's pass
+      // Schedule only: the previous try of this search was screened with a margin m, and
+      // halving α roughly halves it; when m/2 falls below 1.25× the first-level bound that try
+      // had, the first level would almost surely leave this try undecided, so the screen starts
+      // one level finer (it issues the same collectives on every rank: margins and bounds are
+      // reduced statistics). The decision itself is unchanged: every level is rigorous.
+      int level0 = 0;
+      if (pair_k != k && k > 0 && prev_margin > 0.0 && 0.5 * prev_margin < 1.25 * prev_eb0) level0 = 1;
+      if (level0 == 1 && ev_->eval_loss_screen_fine(1, wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) {
+        got = true;
+        via = " (finer first)";
+        eval_ms_ += now_ms() - t0;
+        ++screen_passes_;
+      } else {
+        level0 = 0;
+      }
+      if (got) {
+      } else if (pair_k == k) {  // screened with the previous try's pass
         via = " (paired)";
         ll = pair_ll;
         bnd = pair_bnd;
@@ -937,10 +956,12 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         if (trace_)
           std::fprintf(stderr, "[picard-screen] try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s%s\n", k + 1, alpha,
                        lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb, rejected ? "reject" : "exact", via);
+        prev_margin = lo + eb - current_loss_;
+        if (level0 == 0) prev_eb0 = eb;
         // undecided, but the estimate lies above the current loss (a likely rejection): the
         // finer screens in turn, while the evaluator has them, before the full pass. Their
         // inputs are the reduced statistics, so every rank takes the same branch.
-        for (int level = 1; !rejected && lo + eb > current_loss_; ++level) {
+        for (int level = level0 + 1; !rejected && lo + eb > current_loss_; ++level) {
           const double tf = now_ms();
           if (!ev_->eval_loss_screen_fine(level, wt.data(), n, mu, cfg_.density, ll.data(), bnd.data())) break;
           eval_ms_ += now_ms() - tf;  // device time (host_ms counted it before round 5)
@@ -952,6 +973,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
             eb += std::fabs(signs_[i]) * bnd[i] / (double)T_;
           }
           rejected = !(lo < current_loss_);
+          prev_margin = lo + eb - current_loss_;
           if (trace_)
             std::fprintf(stderr, "[picard-screen] fine%d try %zu alpha %.3e margin %.3e bound %.3e ratio %.3e %s\n", level,
                          k + 1, alpha, lo + eb - current_loss_, eb, (lo + eb - current_loss_) / eb,

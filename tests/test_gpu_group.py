@@ -109,9 +109,9 @@ def test_group_call_sites_match_world1(pa, world):
             assert st["screen_agreed"] == 1 and st["agreements"] >= 1
             for k in want:
                 assert np.array_equal(got[k], res[0][0][k]), (r, k)  # lockstep: identical bits
-                if k == "screen_bound":  # a bound: per-shard rounding slack, ≥ world 1's up to its
-                    # κ1·Σ|ỹ| term, whose fp32 sums group the samples by shard (≤ 2^-22 apart)
-                    assert np.all(got[k] >= want[k] * (1 - 1e-6)), k
+                if k == "screen_bound":  # each shard bounds its own part: the worst-case tail adds
+                    # up to world 1's, the statistical tail (per-shard Cauchy–Schwarz) to about it
+                    assert np.all(got[k] >= want[k] * 0.5) and np.all(got[k] <= want[k] * 4.0), k
                     continue
                 if k == "screen_ll":  # fp32 ℓ: shard-dependent grouping, within the two bounds
                     assert np.all(np.abs(got[k] - want[k]) <= got["screen_bound"] + want["screen_bound"])

@@ -222,10 +222,15 @@ def test_int8_gram_stays_fp64(pa, rng):
 
 @pytest.mark.parametrize("n", [40, 64, 72, 128])
 @pytest.mark.parametrize("dens", [("tanh", 1.0), ("tanh", 0.5), ("exp", 1.0), ("exp", 0.3)])
-def test_screen_bound_holds(pa, rng, n, dens):
+@pytest.mark.parametrize("dmax", ["2", "3"])
+def test_screen_bound_holds(pa, rng, n, dens, dmax, monkeypatch):
     """The line-search screen's bound covers the exact pass: |Σℓ_exact − Σℓ_screen| ≤ bound
-    for every row, over W of very different scales; and it is tight enough to decide
-    (tanh: bound ≤ 1e-4 of Σ|ℓ| with the default D ≤ 3 screen and its fp32 log-likelihood)."""
+    for every row, over W of very different scales, from the first level D ≤ 2 (the default:
+    tanh's fp32 screen; exp runs D ≤ 3) and from D ≤ 3; and at D ≤ 3 it is tight enough to
+    decide (tanh: bound ≤ 1e-4 of Σ|ℓ| with its fp32 log-likelihood; the D ≤ 2 bound's size is
+    checked on the bench mixture, tests/test_gpu_screen_stat.py — the loud sample here inflates
+    its Σ_t 4^e_t)."""
+    monkeypatch.setenv("PICARD_SCREEN_DMAX", dmax)
     x = laplace_mix(rng, n, 20011)
     x[:, 5] *= 1e3  # one loud sample: its exponent dominates its own column only
     ctx = pa.DeviceContext(0)
@@ -241,7 +246,7 @@ def test_screen_bound_holds(pa, rng, n, dens):
         err = np.abs(lo["ll"] - ll_s)
         assert np.all(err <= bnd), (scale, np.max(err / bnd))
         assert np.all(bnd >= 0)
-        if dens[0] == "tanh":
+        if dens[0] == "tanh" and dmax == "3":
             assert np.max(bnd / np.abs(lo["ll"])) <= 1e-4, (scale, np.max(bnd / np.abs(lo["ll"])))
     _, ns = ctx.screen_stats()
     assert ns == 4
