@@ -4008,13 +4008,10 @@ struct DeviceCtx : Evaluator {
     ++n_digit_gram_;
     // Gershgorin: λmax(D_b) ≤ max_f Σ_g |D_b[f][g]|. Tile pair (t1, t2), lane l, reg r holds
     // D_b[fpl·i + t1][fpl·j + t2] with i = 4·(l >> 4) + r, j = l & 15 (and its mirror if t1 ≠ t2)
-    // Planes 0–3 (the pairs that dominate a D ≤ 2 or 3 screen's tail) also get Ostrowski's bound
-    // on the approximate eigenbasis V: λmax(D) ≤ λmax(VᵀDV)/σmin(V)², with λmax(VᵀDV) by
-    // Gershgorin (VᵀDV is nearly diagonal), σmin(V)² ≥ 1 − ‖VᵀV − I‖_F, and 1e-9·tr(D) for the
-    // rounding of VᵀDV (≤ n³·u·tr(D)); the smaller of the two bounds is kept.
-    const int nfp = fpl * 16;
-    std::vector<double> rs(nfp);
-    Mat dm(nfp, nfp);
+    // (An eigenbasis bound — Ostrowski on the approximate eigenvectors — is ≈ 1.2× tighter on the
+    // noise planes and ≈ 1.8× on plane 0, ≈ 18 % off the C3 D ≤ 2 bound; its host eigh costs
+    // 2–15 ms per plane once per image, which a C2 fit of 25 ms cannot afford: not used.)
+    std::vector<double> rs(fpl * 16);
     for (int b = 0; b < OZ_SLICES; ++b) {
       std::fill(rs.begin(), rs.end(), 0.0);
       int p = 0;
@@ -4022,46 +4019,14 @@ struct DeviceCtx : Evaluator {
         for (int t2 = t1; t2 < fpl; ++t2, ++p)
           for (int l = 0; l < 64; ++l)
             for (int r = 0; r < 4; ++r) {
-              const double v = g[((size_t)(b * np + p) * 64 + l) * 4 + r];
+              const double v = std::fabs(g[((size_t)(b * np + p) * 64 + l) * 4 + r]);
               const int i = 4 * (l >> 4) + r, j = l & 15;
-              rs[fpl * i + t1] += std::fabs(v);
-              if (t1 != t2) rs[fpl * j + t2] += std::fabs(v);
-              dm(fpl * i + t1, fpl * j + t2) = v;
-              dm(fpl * j + t2, fpl * i + t1) = v;
+              rs[fpl * i + t1] += v;
+              if (t1 != t2) rs[fpl * j + t2] += v;
             }
       double mx = 0.0;
       for (double v : rs) mx = std::max(mx, v);
       xg_lam_[b] = mx * (1.0 + 1e-12);  // integer sums < 2^53: exact but for the last few adds
-      if (b > 3) continue;
-      std::vector<double> vals;
-      Mat v;
-      eigh(dm, &vals, &v);
-      Mat dv = matmul(dm, v), m(nfp, nfp), vtv(nfp, nfp);
-      for (int i = 0; i < nfp; ++i)
-        for (int j = 0; j < nfp; ++j) {
-          double s = 0.0, u = 0.0;
-          for (int k = 0; k < nfp; ++k) {
-            s += v(k, i) * dv(k, j);
-            u += v(k, i) * v(k, j);
-          }
-          m(i, j) = s;
-          vtv(i, j) = u - (i == j ? 1.0 : 0.0);
-        }
-      double eps = 0.0, tr = 0.0, gm = 0.0;
-      for (int i = 0; i < nfp; ++i) {
-        tr += dm(i, i);
-        double row = 0.0;
-        for (int j = 0; j < nfp; ++j) {
-          eps += vtv(i, j) * vtv(i, j);
-          row += std::fabs(m(i, j));
-        }
-        gm = std::max(gm, row);
-      }
-      eps = std::sqrt(eps) * (1.0 + 1e-6) + 1e-14;
-      if (eps < 0.5 && std::isfinite(gm)) {
-        const double ostrowski = (gm + 1e-9 * tr) / (1.0 - eps) * (1.0 + 1e-12);
-        xg_lam_[b] = std::min(xg_lam_[b], ostrowski);
-      }
     }
     xg_valid_ = true;
     return true;
