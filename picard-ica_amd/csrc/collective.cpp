@@ -257,7 +257,10 @@ class RcclCollective final : public Collective {
         last_probe = now;
         probe(secs_since(t0));
       }
-      if (spin < 4096) sched_yield();
+      // yield between probes while a pass can still be running (C3's longest shard pass is
+      // ≈ 10 ms at 8 ranks, 75 ms at 1); a usleep wakes 20–70 µs late, a cost every pass paid
+      // once the old cap of 4096 yields (a few ms) was spent. Past 0.5 s (a slow peer) sleep.
+      if (spin < 1024 || secs_since(t0) < 0.5) sched_yield();
       else usleep(20);
     }
     check();

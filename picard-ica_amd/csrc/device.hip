@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <sched.h>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -2811,10 +2812,33 @@ struct DeviceCtx : Evaluator {
     if (coll_) {
       coll_->wait(stream);
       harvest_allreduce_timing();
+    } else if (sync_poll_) {
+      // poll the stream (yielding the core to any runnable thread between probes): a blocking
+      // hipStreamSynchronize wakes ≈ 12 µs after the work ends, a cost every pass pays once —
+      // C2-shaped fits are launch-bound (profiles/r06_y/ab_sync_poll.log: N = 64, T = 1e6
+      // 0.80 → 0.75 ms per step). Past 0.5 s (setup kernels, JADE) the blocking wait takes over.
+      const double t0 = now_ms_d();
+      hipError_t e;
+      for (uint32_t k = 0; (e = hipStreamQuery(stream)) == hipErrorNotReady; ++k) {
+        if ((k & 1023u) == 1023u && now_ms_d() - t0 > 500.0) {
+          e = hipStreamSynchronize(stream);
+          break;
+        }
+        sched_yield();
+      }
+      HIP_OK(e);
     } else {
       HIP_OK(hipStreamSynchronize(stream));
     }
   }
+  static double now_ms_d() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  // PICARD_SYNC_POLL=0: every wait on the context's stream is a blocking hipStreamSynchronize
+  const bool sync_poll_ = [] {
+    const char* e = std::getenv("PICARD_SYNC_POLL");
+    return !(e && std::atoi(e) == 0);
+  }();
   // Time inside the all-reduces (bench.py's per-rank report): RCCL — device time between HIP
   // events around each ncclAllReduce on the stream (the kernel waits there for the slowest
   // rank); in-process group — host time of the exchange. Events come from a ring, read back
