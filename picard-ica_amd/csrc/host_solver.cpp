@@ -917,13 +917,22 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         bnd = pair_bnd;
         pair_k = tries;
         got = true;
-      } else if (first_loss_only && pairs_ok_ && k + 1 < tries && ahead_ &&
-                 !(ls_curv_ > 0.0 && curvature_lower_bound(alpha / 2.0) > ls_slack_)) {
+      } else if (pairs_ok_ && k + 1 < tries && ahead_ &&
+                 (first_loss_only ? !(ls_curv_ > 0.0 && curvature_lower_bound(alpha / 2.0) > ls_slack_)
+                                  : descent_pair_ && !full_first && pred_slope_ < 0.0 && pred_qh_ > 0.0 &&
+                                        0.5 * alpha >= 8.0 * -pred_slope_ / pred_qh_ &&
+                                        (k == 0 || (prev_margin > 0.0 && 0.25 * prev_margin > 2.5 * prev_eb0)))) {
         // Schedule only: a non-descent direction (⟨g, D⟩ ≥ 0) almost surely fails every try,
         // and its next try will be screened too (not rejected by curvature), so both tries go
         // in one pass — half the bytes per try for a screen whose clock the memory side's power
         // holds down. Each try's rows are those of its own screen (the same
         // arithmetic per W), so every decision is unchanged.
+        // An overshooting descent search pairs its tries the same way while Picard's quadratic
+        // model puts the loss's zero crossing α₀ = 2|slope|/qh at most a quarter of the next try's α
+        // (so neither try is predicted to descend, and the next try takes no model full pass)
+        // and the previous try's margin, at least halving per try, leaves the next one decided
+        // at the first level with room (m/4 > 2.5× its bound). C3's two overshooting searches
+        // (7 rejected tries each) ran 7 single screens. PICARD_DESCENT_PAIR=0: singles.
         const Mat wt2 = matmul(ahead_->get(k + 1, &ahead_wait_ms_), P_);
         pair_ll.assign(n, 0.0);
         pair_bnd.assign(n, 0.0);

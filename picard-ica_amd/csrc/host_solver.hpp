@@ -1,6 +1,7 @@
 // Host Picard driver: src/solver.rs:45-249 + src/core.rs:162-401 +
 // src/lbfgs.rs:84-171 + src/jade.rs:22-197 restated over an Evaluator.
 #pragma once
+#include <cstdlib>
 #include <deque>
 #include <limits>
 #include <memory>
@@ -150,6 +151,11 @@ class Solver {
   int first_cell_ = 0;
   // the model along this iteration's D (slope, qh) and the later-try cell's counts
   double pred_slope_ = 0.0, pred_qh_ = 0.0, later_n_ = 0.0, later_acc_ = 0.0;
+  // pair the screens of an overshooting descent search (line_search; PICARD_DESCENT_PAIR=0: off)
+  const bool descent_pair_ = [] {
+    const char* e = std::getenv("PICARD_DESCENT_PAIR");
+    return !(e && std::atoi(e) == 0);
+  }();
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are
