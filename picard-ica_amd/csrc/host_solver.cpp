@@ -940,7 +940,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
                                    pair_bnd.data())) {
           pair_k = k + 1;
           ++screen_pairs_;
-          via = " (pair)";
+          via = first_loss_only ? " (pair)" : " (pair, descent)";
           got = true;
           eval_ms_ += now_ms() - t0;
           ++screen_passes_;

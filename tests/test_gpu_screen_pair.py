@@ -63,3 +63,30 @@ def test_paired_fit_bit_identical(pa, n, seed, capfd, monkeypatch):
             assert "(pair)" not in err and "(paired)" not in err
     assert res["1"].n_iterations == res["0"].n_iterations and res["1"].converged == res["0"].converged
     assert np.array_equal(res["1"].unmixing, res["0"].unmixing)
+
+
+@pytest.mark.parametrize("n,t,seed", [(128, 1000003, 42)])
+def test_descent_paired_fit_bit_identical(pa, n, t, seed, capfd, monkeypatch):
+    """Overshooting descent searches pair their screens (Solver::line_search: Picard's quadratic
+    model and the previous try's margin decide, schedule only); with PICARD_DESCENT_PAIR=0 they
+    run single screens. Identical iterations, bit-identical unmixing, and descent pairs ran."""
+    monkeypatch.setenv("PICARD_TRACE", "1")
+    res = {}
+    for pairs in ("1", "0"):
+        monkeypatch.setenv("PICARD_DESCENT_PAIR", pairs)
+        ctx = pa.DeviceContext(0)
+        ctx.generate(n, t, seed)
+        sv = pa.Solver(ctx, pa.PicardConfig(random_state=42, max_iter=60))
+        while not sv.step():
+            pass
+        res[pairs] = sv.finish()
+        sv.close()
+        ctx.close()
+        err = capfd.readouterr().err
+        print(pairs, err.count("(pair, descent)"))
+        if pairs == "1":
+            assert "(pair, descent)" in err
+        else:
+            assert "(pair, descent)" not in err
+    assert res["1"].n_iterations == res["0"].n_iterations and res["1"].converged == res["0"].converged
+    assert np.array_equal(res["1"].unmixing, res["0"].unmixing)
