@@ -126,8 +126,8 @@ def test_group_fit_reproduces_world1(pa, world, capfd, monkeypatch):
     """The rank-replicated Solver over the group, Picard-O at N = 128 on the int8 Y stage
     with the line-search screen and the curvature rejection (the bench's C3 path):
     every rank bit-identical, and the same iteration count as world = 1 with the
-    unmixing within 1e-10; the screen agreement ran, and so did the screen and the
-    curvature rejection."""
+    unmixing within 1e-10; the screen agreement ran, and so did the screen, the descent-search
+    screen pairs and the curvature rejection."""
     monkeypatch.setenv("PICARD_TRACE", "1")
     nf, T = 128, 200003
     cfg = pa.PicardConfig(random_state=42, max_iter=40, want_sources=False)
@@ -168,6 +168,7 @@ def test_group_fit_reproduces_world1(pa, world, capfd, monkeypatch):
     assert np.max(np.abs(r0.unmixing - ref.unmixing)) <= 1e-10
     assert np.max(np.abs(r0.whitening - ref.whitening)) <= 1e-10
     assert "[picard-screen]" in trace and "[picard-curv]" in trace
+    assert "(pair, descent)" in trace  # descent-search screen pairs ran on every rank alike
 
 
 def test_group_nonortho_fit_rank_identical(pa):
