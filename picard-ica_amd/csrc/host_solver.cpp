@@ -920,7 +920,7 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
       } else if (pairs_ok_ && k + 1 < tries && ahead_ &&
                  (first_loss_only ? !(ls_curv_ > 0.0 && curvature_lower_bound(alpha / 2.0) > ls_slack_)
                                   : descent_pair_ && !full_first && pred_slope_ < 0.0 && pred_qh_ > 0.0 &&
-                                        0.5 * alpha >= 8.0 * -pred_slope_ / pred_qh_ &&
+                                        0.5 * alpha >= descent_pair_factor_ * -pred_slope_ / pred_qh_ &&
                                         (k == 0 || (prev_margin > 0.0 && 0.25 * prev_margin > 2.5 * prev_eb0)))) {
         // Schedule only: a non-descent direction (⟨g, D⟩ ≥ 0) almost surely fails every try,
         // and its next try will be screened too (not rejected by curvature), so both tries go
@@ -929,7 +929,8 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         // arithmetic per W), so every decision is unchanged.
         // An overshooting descent search pairs its tries the same way while Picard's quadratic
         // model puts the loss's zero crossing α₀ = 2|slope|/qh at most a quarter of the next try's α
-        // (so neither try is predicted to descend, and the next try takes no model full pass)
+        // (so neither try is predicted to descend, and the next try takes no model full pass; on C3
+        // the accepted try of a descent search lay within 2.5·α₀, the pair's first try is ≥ 8·α₀)
         // and the previous try's margin, at least halving per try, leaves the next one decided
         // at the first level with room (m/4 > 2.5× its bound). C3's two overshooting searches
         // (7 rejected tries each) ran 7 single screens. PICARD_DESCENT_PAIR=0: singles.

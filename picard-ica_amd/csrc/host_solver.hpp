@@ -156,6 +156,12 @@ class Solver {
     const char* e = std::getenv("PICARD_DESCENT_PAIR");
     return !(e && std::atoi(e) == 0);
   }();
+  // the pair's second try lies at ≥ factor·|slope|/qh (PICARD_DESCENT_PAIR_FACTOR; 8 = 4·α₀)
+  const double descent_pair_factor_ = [] {
+    const char* e = std::getenv("PICARD_DESCENT_PAIR_FACTOR");
+    const double f = e ? std::atof(e) : 8.0;
+    return f >= 2.0 ? f : 8.0;
+  }();
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
   // the bench data, and then its G is the next gradient); tries ≥ 2 are
