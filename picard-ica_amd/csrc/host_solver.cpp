@@ -928,9 +928,9 @@ Solver::LsResult Solver::line_search(const Mat& direction, size_t tries, bool mu
         // holds down. Each try's rows are those of its own screen (the same
         // arithmetic per W), so every decision is unchanged.
         // An overshooting descent search pairs its tries the same way while Picard's quadratic
-        // model puts the loss's zero crossing α₀ = 2|slope|/qh at most a quarter of the next try's α
-        // (so neither try is predicted to descend, and the next try takes no model full pass; on C3
-        // the accepted try of a descent search lay within 2.5·α₀, the pair's first try is ≥ 8·α₀)
+        // model puts the loss's zero crossing α₀ = 2|slope|/qh at most half the next try's α (so
+        // neither try is predicted to descend, and the next try takes no model full pass; on C3 the
+        // accepted try of a descent search lay within 2.5·α₀, the pair's first try is ≥ 4·α₀)
         // and the previous try's margin, at least halving per try, leaves the next one decided
         // at the first level with room (m/4 > 2.5× its bound). C3's two overshooting searches
         // (7 rejected tries each) ran 7 single screens. PICARD_DESCENT_PAIR=0: singles.

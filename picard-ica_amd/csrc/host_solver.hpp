@@ -156,11 +156,12 @@ class Solver {
     const char* e = std::getenv("PICARD_DESCENT_PAIR");
     return !(e && std::atoi(e) == 0);
   }();
-  // the pair's second try lies at ≥ factor·|slope|/qh (PICARD_DESCENT_PAIR_FACTOR; 8 = 4·α₀)
+  // the pair's second try lies at ≥ factor·|slope|/qh (PICARD_DESCENT_PAIR_FACTOR; 4 = 2·α₀:
+  // C3 screens 20.6 → 20.3 ms per step against 8, profiles/r06_final/ab_descent_pair_factor.log)
   const double descent_pair_factor_ = [] {
     const char* e = std::getenv("PICARD_DESCENT_PAIR_FACTOR");
-    const double f = e ? std::atof(e) : 8.0;
-    return f >= 2.0 ? f : 8.0;
+    const double f = e ? std::atof(e) : 4.0;
+    return f >= 2.0 ? f : 4.0;
   }();
   // Evaluation schedule of a line search (results are bit-identical whatever
   // the schedule): try 1 is a full fused pass (accepted ≈ 80 % of the time on
